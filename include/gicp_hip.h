@@ -1,0 +1,137 @@
+/*
+ * gicp_hip.h — C-ABI of libgicp_hip.so, the MI355X (gfx950) GICP engine.
+ *
+ * The drop-in boundary for the reference's only public surface,
+ *   gicp(source_points, target_points, max_iterations=100, tolerance=1e-6,
+ *        max_distance_correspondence=150, max_distance_nearest_neighbors=50)
+ *   (/root/reference/python-implementation/gicp.py:78, returns gicp.py:174)
+ * and apply_transformation(cloud, T) (gicp.py:176-177).  The Python module
+ * generalized-icp_amd/gicp/__init__.py binds these entry points with ctypes
+ * and restores the reference's signature and 7-tuple; INTEGRATION.md shows
+ * the binding.
+ *
+ * Conventions
+ *   - Host buffers are caller-owned, fp64, row-major (N x dim); device
+ *     buffers are library-owned.  No torch / HIP types cross this boundary.
+ *   - Every int-returning call returns GICP_OK (0) or a negative GICP_E_*;
+ *     gicp_last_error() then describes the failure.  No C++ exception
+ *     crosses the boundary.
+ *   - HIP is initialised lazily inside gicp_create(), never at load time, so
+ *     the library is safe to load before fork() (robot-visualization.py:199
+ *     runs gicp() in a forked worker).
+ *   - One context = one GPU = one host thread; one process per GPU.  Ranks
+ *     of a multi-GPU job share the per-iteration statistics through an RCCL
+ *     all-reduce (gicp_comm_init); every rank then runs the same host solve.
+ */
+#ifndef GICP_HIP_H
+#define GICP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GICP_OK 0
+#define GICP_E_INVALID (-1)   /* bad argument (shape, dim, NULL, range) */
+#define GICP_E_HIP (-2)       /* HIP runtime failure */
+#define GICP_E_STATE (-3)     /* call out of order (e.g. align before set_target) */
+#define GICP_E_COMM (-4)      /* RCCL failure */
+#define GICP_E_NOMEM (-5)     /* host or device allocation failed */
+
+#define GICP_COMM_ID_BYTES 128
+#define GICP_MAX_STATS 74     /* statistics per pass, dim 3 (dim 2: 26) */
+
+typedef struct gicp_ctx gicp_ctx;
+
+/* Keyword arguments of gicp() (gicp.py:78) and the constants gicp.py
+ * hard-codes (epsilon gicp.py:5, 0.1 ratio gicp.py:11, k = 6 gicp.py:24). */
+typedef struct gicp_params {
+    int32_t max_iterations;                 /* gicp.py:78, default 100 */
+    int32_t k_neighbors;                    /* 0 -> 6 for dim 2 (gicp.py:24), 20 for dim 3 */
+    double tolerance;                       /* |delta loss| < tolerance stops, gicp.py:155-162 */
+    double max_distance_correspondence;     /* d_c, inclusive (gicp.py:136), default 150 */
+    double max_distance_nearest_neighbors;  /* d_n, strict (KDTree distance_upper_bound, gicp.py:24), default 50 */
+    double epsilon;                         /* 100 (gicp.py:5) */
+    double ratio;                           /* 0.1 (gicp.py:11) */
+    int32_t fixed_iterations;               /* 1: never stop on tolerance (benchmark mode) */
+    int32_t min_neighbors;                  /* 0 -> dim (2-D: > 1 neighbour, gicp.py:27) */
+} gicp_params;
+
+/* What gicp_align() reports (the reference only prints "Converged at iteration", gicp.py:161). */
+typedef struct gicp_result {
+    int32_t iterations;        /* outer iterations executed (each = correspondences + solve) */
+    int32_t converged;         /* 1 if |delta loss| < tolerance stopped the loop */
+    int32_t converged_at;      /* iteration index printed by gicp.py:161, -1 if none */
+    int32_t ambiguous;         /* points re-resolved in fp64 in the last pass (diagnostic) */
+    double final_loss;         /* min_loss of the last inner solve */
+    int64_t correspondences;   /* accepted correspondences in the last pass, all ranks */
+    double wall_ms;            /* host wall time of the iteration loop */
+    double corr_kernel_ms;     /* sum of HIP-event durations of the correspondence kernel */
+    double reduce_ms;          /* sum of HIP-event durations of partial-reduce + all-reduce */
+    int64_t pairs_evaluated;   /* source x target distance evaluations in the last pass (if counted) */
+} gicp_result;
+
+/* Optional caller-allocated per-point outputs of one pass, ORIGINAL source
+ * order, this rank's shard only (other rows untouched).  Any pointer may be NULL. */
+typedef struct gicp_debug {
+    int64_t* index;      /* [N] target index of the correspondence, -1 if rejected (gicp.py:136-138) */
+    double* weight;      /* [N, dim, dim] W_i = inv(R C_s R^T + C_t), zeros if rejected (gicp.py:143-145) */
+    double* distance;    /* [N] fp64 distance to the nearest target point (gicp.py:133) */
+} gicp_debug;
+
+/* ---- library ------------------------------------------------------------ */
+int gicp_version(void);                          /* 100 * major + minor */
+int gicp_stats_size(int dim);                    /* 26 (dim 2) or 74 (dim 3) */
+void gicp_default_params(int dim, gicp_params* out);
+const char* gicp_strerror(int code);
+
+/* ---- context ------------------------------------------------------------ */
+int gicp_create(gicp_ctx** out, int device);     /* lazily initialises HIP on `device` */
+void gicp_destroy(gicp_ctx* ctx);
+const char* gicp_last_error(const gicp_ctx* ctx);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI ---------------------- */
+int gicp_comm_unique_id(char out[GICP_COMM_ID_BYTES]);   /* rank 0, then broadcast out-of-band */
+int gicp_comm_init(gicp_ctx* ctx, int nranks, int rank, const char id[GICP_COMM_ID_BYTES]);
+
+/* ---- clouds -------------------------------------------------------------- */
+/* Target cloud (gicp.py:101,104): builds the tile index and the per-point
+ * surface covariances once; reusable across gicp_align calls. */
+int gicp_set_target(gicp_ctx* ctx, const double* xyz, int64_t M, int dim, const gicp_params* p);
+/* Source cloud (gicp.py:100,111): the whole cloud is uploaded (its
+ * covariance neighbourhoods need every point); this rank reduces only the
+ * points of shard `rank` of `nshards` (Morton-contiguous tiles). */
+int gicp_set_source(gicp_ctx* ctx, const double* xyz, int64_t N, int dim, const gicp_params* p,
+                    int shard, int nshards);
+/* Promote the current target (index + covariances) to be the next source,
+ * as robot-visualization.py:250 swaps scans; then set a new target. */
+int gicp_target_to_source(gicp_ctx* ctx, int shard, int nshards);
+
+/* Surface covariances C = a I - m m^T of the last set_target/set_source,
+ * original order, [n, dim, dim] (gicp.py:104 target_cov_matrices, :111
+ * initial_source_cov_matrices).  which: 0 = target, 1 = source. */
+int gicp_get_covariances(gicp_ctx* ctx, int which, double* out);
+/* Neighbour count (incl. self, < d_n, capped at k) per point, original order. */
+int gicp_get_neighbor_counts(gicp_ctx* ctx, int which, int32_t* out);
+
+/* ---- the hot path -------------------------------------------------------- */
+/* One pass at pose T ((dim+1)^2, row-major): correspondences + Mahalanobis
+ * weights + normal-equation statistics (gicp.py:119-145 plus everything
+ * loss()/grad_loss() need, gicp.py:52-76).  `stats` receives
+ * gicp_stats_size(dim) doubles, summed over all ranks when a communicator is
+ * set.  Layout: see DESIGN.md §4 (A, B, C, gR, gt, c0, count). */
+int gicp_iterate(gicp_ctx* ctx, const double* T, double* stats, gicp_debug* dbg);
+
+/* Host solve of the inner problem (gicp.py:148-154): minimise
+ * c0 - 2 g^T dz + dz^T H dz over SE(dim), dz = z(T) - z(T_k), starting at T_k.
+ * Pure host code, no GPU needed.  Writes T_out and the minimum. */
+int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_out, double* loss_out);
+
+/* The whole outer loop (gicp.py:116-167) on the GPU + host solver. */
+int gicp_align(gicp_ctx* ctx, const double* T0, const gicp_params* p, double* T_out, gicp_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GICP_HIP_H */
