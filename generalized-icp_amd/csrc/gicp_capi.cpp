@@ -1,0 +1,695 @@
+// gicp_capi.cpp — the C-ABI of libgicp_hip.so (include/gicp_hip.h).
+//
+// Owns one GPU per context: device copies of both clouds (Morton-sorted tile index,
+// per-point surface covariances), the per-iteration workspace, an optional RCCL
+// communicator for the statistics all-reduce, and the outer loop of gicp.py:116-167.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <new>
+#include <string>
+#include <vector>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "../../include/gicp_hip.h"
+#include "gicp_internal.h"
+
+namespace gicp {
+hipError_t launch_morton(const double*, int64_t, int, const DevCloud&, uint32_t*, int32_t*, hipStream_t);
+hipError_t launch_build_tiles(const double*, int, const int32_t*, TileInfo*, int, double*, float4*, int32_t*,
+                              unsigned*, hipStream_t);
+hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
+hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
+hipError_t launch_corr(const CorrArgs&, int, hipStream_t);
+hipError_t launch_reduce(const double*, int, int, double*, hipStream_t);
+int corr_grid(int);
+int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
+}  // namespace gicp
+
+using namespace gicp;
+
+namespace {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) throw Fail{GICP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+template <class T>
+void dalloc(T*& p, size_t n) {
+    if (p) {
+        (void)hipFree(p);
+        p = nullptr;
+    }
+    if (n == 0) n = 1;
+    HIPCHK(hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T)));
+}
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+// One indexed cloud on the device.
+struct Cloud {
+    int dim = 0;
+    int64_t n = 0;
+    int ntiles = 0, nblocks = 0, level = 0, bits = 0;
+    double lo[3] = {0, 0, 0};
+    double scale = 1.0;
+    float rho = 0.f;
+    double* xyz64 = nullptr;
+    float4* rel32 = nullptr;
+    double4* cov = nullptr;
+    int32_t* perm = nullptr;
+    int32_t* inv = nullptr;
+    int32_t* ncount = nullptr;
+    TileInfo* tiles = nullptr;
+    BlockInfo* blocks = nullptr;
+    uint32_t* tile_code = nullptr;
+    bool cov_ready = false;
+    int cov_q_begin = 0, cov_q_end = 0;  // tiles whose covariances were computed
+
+    void release() {
+        dfree(xyz64);
+        dfree(rel32);
+        dfree(cov);
+        dfree(perm);
+        dfree(inv);
+        dfree(ncount);
+        dfree(tiles);
+        dfree(blocks);
+        dfree(tile_code);
+        n = 0;
+        cov_ready = false;
+    }
+    DevCloud view() const {
+        DevCloud v{};
+        v.xyz64 = xyz64;
+        v.rel32 = rel32;
+        v.cov = cov;
+        v.perm = perm;
+        v.tiles = tiles;
+        v.blocks = blocks;
+        v.tile_code = tile_code;
+        v.n = n;
+        v.ntiles = ntiles;
+        v.nblocks = nblocks;
+        for (int a = 0; a < 3; ++a) v.lo[a] = lo[a];
+        v.scale = scale;
+        v.bits = bits;
+        v.dim = dim;
+        return v;
+    }
+};
+
+}  // namespace
+
+struct gicp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    Cloud tgt, src;
+    gicp_params ptgt{}, psrc{};
+    int shard = 0, nshards = 1, q_begin = 0, q_end = 0;
+    int32_t* d_hint = nullptr;
+    double* d_partials = nullptr;
+    size_t partials_cap = 0;
+    double* d_stats = nullptr;
+    double* h_stats = nullptr;
+    int32_t* d_amb = nullptr;
+    int64_t* d_dbg_idx = nullptr;
+    double* d_dbg_w = nullptr;
+    double* d_dbg_dist = nullptr;
+    size_t dbg_cap = 0;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // diagnostics of the last pass
+    double last_amb = 0.0, last_pairs = 0.0;
+    float last_corr_ms = 0.f, last_reduce_ms = 0.f;
+    bool timing = false;
+};
+
+namespace {
+
+void default_params(int dim, gicp_params* p) {
+    std::memset(p, 0, sizeof(*p));
+    p->max_iterations = 100;
+    p->k_neighbors = dim == 2 ? 6 : 20;
+    p->tolerance = 1e-6;
+    p->max_distance_correspondence = 150.0;
+    p->max_distance_nearest_neighbors = 50.0;
+    p->epsilon = 100.0;
+    p->ratio = 0.1;
+    p->fixed_iterations = 0;
+    p->min_neighbors = dim;
+}
+
+gicp_params resolve(int dim, const gicp_params* in) {
+    gicp_params p;
+    default_params(dim, &p);
+    if (!in) return p;
+    p = *in;
+    if (p.k_neighbors <= 0) p.k_neighbors = dim == 2 ? 6 : 20;
+    if (p.min_neighbors <= 0) p.min_neighbors = dim;
+    if (p.epsilon == 0.0) p.epsilon = 100.0;
+    return p;
+}
+
+// fp32-screen error bound: E bounds the error of one coordinate difference
+Margin make_margin(int dim, float rho_q, float rho_db, double dmax) {
+    const double E = std::ldexp(8.0 * rho_q + 3.0 * rho_db + 3.0 * dmax, -23) + 1e-30;
+    Margin m;
+    m.a = (float)(2.0 * std::sqrt((double)dim) * E);
+    m.b = (float)(dim * E * E);
+    m.c = (float)std::ldexp(1.0, -16);
+    return m;
+}
+float screen_bound(const Margin& m, double d) {
+    const double d2 = d * d;
+    const double b = d2 + 2.0 * (m.a * d + m.b + m.c * d2);
+    return (float)(b * (1.0 + 1e-6)) + 1e-30f;
+}
+
+// Choose the finest Morton level whose cell-bounded tiles stay <= 1.3x the minimum count.
+void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
+                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& level_out) {
+    const int64_t n = (int64_t)codes.size();
+    const double target = 1.3 * std::ceil(n / 64.0) + 2.0;
+    int level = 0;
+    for (int lv = bits; lv >= 0; --lv) {
+        const int shift = dim * (bits - lv);
+        int64_t nt = 0, run = 1;
+        for (int64_t i = 1; i <= n; ++i) {
+            if (i == n || (shift >= 32 ? 0u : (codes[i] >> shift)) != (shift >= 32 ? 0u : (codes[i - 1] >> shift))) {
+                nt += (run + 63) / 64;
+                run = 1;
+            } else {
+                ++run;
+            }
+        }
+        if (nt <= target) {
+            level = lv;
+            break;
+        }
+    }
+    level_out = level;
+    const int shift = dim * (bits - level);
+    start.clear();
+    count.clear();
+    first_code.clear();
+    int64_t i0 = 0;
+    for (int64_t i = 1; i <= n; ++i) {
+        const bool brk = i == n || (shift >= 32 ? false : (codes[i] >> shift) != (codes[i - 1] >> shift));
+        if (brk || i - i0 == 64) {
+            start.push_back((int32_t)i0);
+            count.push_back((int32_t)(i - i0));
+            first_code.push_back(codes[i0]);
+            i0 = i;
+        }
+    }
+}
+
+// Build the device index of a cloud and its per-point covariances for tiles [qb, qe) (qe < 0: all).
+void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, int shard,
+                 int nshards, bool cov_all) {
+    if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
+    if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
+    for (int64_t i = 0; i < n * dim; ++i)
+        if (!std::isfinite(xyz[i])) throw Fail{GICP_E_INVALID, "cloud contains non-finite coordinates"};
+    cl.release();
+    cl.dim = dim;
+    cl.n = n;
+    cl.bits = dim == 3 ? 10 : 16;
+    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    for (int a = 0; a < dim; ++a) {
+        mn[a] = mx[a] = xyz[a];
+    }
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < dim; ++a) {
+            mn[a] = std::min(mn[a], xyz[i * dim + a]);
+            mx[a] = std::max(mx[a], xyz[i * dim + a]);
+        }
+    double ext = 0.0;
+    for (int a = 0; a < dim; ++a) ext = std::max(ext, mx[a] - mn[a]);
+    ext = ext * (1.0 + 1e-9) + 1e-12 * (1.0 + std::fabs(mn[0]));
+    for (int a = 0; a < 3; ++a) cl.lo[a] = a < dim ? mn[a] : 0.0;
+    cl.scale = std::ldexp(1.0, cl.bits) / ext;
+
+    hipStream_t st = c->stream;
+    double* d_in = nullptr;
+    uint32_t *d_codes = nullptr, *d_codes_s = nullptr;
+    int32_t* d_idx = nullptr;
+    void* d_tmp = nullptr;
+    try {
+        dalloc(d_in, (size_t)n * dim);
+        HIPCHK(hipMemcpyAsync(d_in, xyz, sizeof(double) * n * dim, hipMemcpyHostToDevice, st));
+        dalloc(d_codes, n);
+        dalloc(d_codes_s, n);
+        dalloc(d_idx, n);
+        dalloc(cl.perm, n);
+        DevCloud fr = cl.view();
+        HIPCHK(launch_morton(d_in, n, dim, fr, d_codes, d_idx, st));
+        size_t tmp_bytes = 0;
+        const unsigned end_bit = (unsigned)(dim * cl.bits);
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
+                                         st));
+        HIPCHK(hipMalloc(&d_tmp, tmp_bytes + 16));
+        HIPCHK(rocprim::radix_sort_pairs(d_tmp, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
+                                         st));
+        std::vector<uint32_t> codes(n);
+        HIPCHK(hipMemcpyAsync(codes.data(), d_codes_s, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<int32_t> tstart, tcount;
+        std::vector<uint32_t> tcode;
+        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level);
+        cl.ntiles = (int)tstart.size();
+        cl.nblocks = (cl.ntiles + kBlockTiles - 1) / kBlockTiles;
+        std::vector<TileInfo> ti(cl.ntiles);
+        std::memset(ti.data(), 0, sizeof(TileInfo) * ti.size());
+        for (int t = 0; t < cl.ntiles; ++t) {
+            ti[t].start = tstart[t];
+            ti[t].count = tcount[t];
+        }
+        dalloc(cl.tiles, cl.ntiles);
+        dalloc(cl.blocks, cl.nblocks);
+        dalloc(cl.tile_code, cl.ntiles);
+        dalloc(cl.xyz64, (size_t)n * 4);
+        dalloc(cl.rel32, n);
+        dalloc(cl.inv, n);
+        dalloc(cl.cov, n);
+        dalloc(cl.ncount, n);
+        unsigned* d_rho = reinterpret_cast<unsigned*>(d_codes);  // reuse scratch
+        HIPCHK(hipMemsetAsync(d_rho, 0, sizeof(unsigned), st));
+        HIPCHK(hipMemcpyAsync(cl.tiles, ti.data(), sizeof(TileInfo) * cl.ntiles, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(cl.tile_code, tcode.data(), sizeof(uint32_t) * cl.ntiles, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_build_tiles(d_in, dim, cl.perm, cl.tiles, cl.ntiles, cl.xyz64, cl.rel32, cl.inv, d_rho, st));
+        HIPCHK(launch_build_blocks(cl.tiles, cl.ntiles, cl.blocks, cl.nblocks, dim, st));
+        unsigned rho_bits = 0;
+        HIPCHK(hipMemcpyAsync(&rho_bits, d_rho, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::memcpy(&cl.rho, &rho_bits, sizeof(float));
+
+        // surface covariances (gicp.py:19-35) for this rank's query tiles
+        int qb = 0, qe = cl.ntiles;
+        if (!cov_all) {
+            qb = (int)((int64_t)cl.ntiles * shard / nshards);
+            qe = (int)((int64_t)cl.ntiles * (shard + 1) / nshards);
+        }
+        CovArgs ca{};
+        ca.cl = cl.view();
+        ca.q_begin = qb;
+        ca.q_end = qe;
+        const double dn = p.max_distance_nearest_neighbors;
+        ca.mg = make_margin(dim, cl.rho, cl.rho, dn);
+        ca.search2 = screen_bound(ca.mg, dn);
+        ca.dn2 = dn * dn;
+        ca.eps_a = p.epsilon;
+        ca.m_scale = std::sqrt(p.epsilon * (1.0 - p.ratio));
+        ca.min_nb = p.min_neighbors;
+        ca.cov_out = cl.cov;
+        ca.count_out = cl.ncount;
+        ca.amb_counter = c->d_amb;
+        HIPCHK(hipMemsetAsync(cl.ncount, 0, sizeof(int32_t) * n, st));
+        hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, st);
+        if (e == hipErrorInvalidValue) throw Fail{GICP_E_INVALID, "unsupported k_neighbors for this dim (2-D: 6, 10; 3-D: 10, 20)"};
+        HIPCHK(e);
+        HIPCHK(hipStreamSynchronize(st));
+        cl.cov_ready = true;
+        cl.cov_q_begin = qb;
+        cl.cov_q_end = qe;
+    } catch (...) {
+        dfree(d_in);
+        dfree(d_codes);
+        dfree(d_codes_s);
+        dfree(d_idx);
+        if (d_tmp) (void)hipFree(d_tmp);
+        throw;
+    }
+    dfree(d_in);
+    dfree(d_codes);
+    dfree(d_codes_s);
+    dfree(d_idx);
+    (void)hipFree(d_tmp);
+}
+
+void set_shard(gicp_ctx* c, int shard, int nshards) {
+    if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
+    c->shard = shard;
+    c->nshards = nshards;
+    c->q_begin = (int)((int64_t)c->src.ntiles * shard / nshards);
+    c->q_end = (int)((int64_t)c->src.ntiles * (shard + 1) / nshards);
+    dalloc(c->d_hint, std::max(1, c->src.ntiles));
+    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * std::max(1, c->src.ntiles), c->stream));
+}
+
+void ensure_workspace(gicp_ctx* c) {
+    const int nsx = nstat_ext(3);
+    const size_t need = (size_t)std::max(1, corr_grid(c->q_end - c->q_begin)) * nsx;
+    if (need > c->partials_cap) {
+        dalloc(c->d_partials, need);
+        c->partials_cap = need;
+    }
+    if (!c->d_stats) dalloc(c->d_stats, nsx);
+    if (!c->h_stats) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_stats), sizeof(double) * nsx));
+}
+
+// One pass at pose T: statistics (all-reduced) into c->h_stats.
+void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
+    if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
+    if (c->tgt.dim != c->src.dim) throw Fail{GICP_E_INVALID, "source and target dimensions differ"};
+    const int d = c->src.dim, n1 = d + 1;
+    ensure_workspace(c);
+    CorrArgs a{};
+    a.src = c->src.view();
+    a.tgt = c->tgt.view();
+    a.q_begin = c->q_begin;
+    a.q_end = c->q_end;
+    for (int r = 0; r < d; ++r) {
+        for (int k = 0; k < d; ++k) {
+            a.R[r * d + k] = T[r * n1 + k];
+            a.R32[r * d + k] = (float)T[r * n1 + k];
+        }
+        a.t[r] = T[r * n1 + d];
+    }
+    for (int k = 0; k < d * n1 + n1; ++k)
+        if (!std::isfinite(T[k])) throw Fail{GICP_E_INVALID, "pose contains non-finite values"};
+    const double dc = c->psrc.max_distance_correspondence;
+    a.dc = dc;
+    a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc);
+    a.search2 = screen_bound(a.mg, dc);
+    a.hint = c->d_hint;
+    a.partials = c->d_partials;
+    a.count_pairs = 1;
+    if (dbg && (dbg->index || dbg->weight || dbg->distance)) {
+        const size_t n = (size_t)c->src.n;
+        if (c->dbg_cap < n) {
+            dalloc(c->d_dbg_idx, n);
+            dalloc(c->d_dbg_w, n * d * d);
+            dalloc(c->d_dbg_dist, n);
+            c->dbg_cap = n;
+        }
+        a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
+        a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
+        a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
+    }
+    const int nsx = nstat_ext(d);
+    const int grid = corr_grid(c->q_end - c->q_begin);
+    hipStream_t st = c->stream;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], st));
+    if (grid > 0) HIPCHK(launch_corr(a, d, st));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], st));
+    if (grid > 0) HIPCHK(launch_reduce(c->d_partials, grid, nsx, c->d_stats, st));
+    else HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(double) * nsx, st));
+    if (c->comm) {
+        ncclResult_t r = ncclAllReduce(c->d_stats, c->d_stats, nsx, ncclFloat64, ncclSum, c->comm, st);
+        if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+    }
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], st));
+    HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, st));
+    if (dbg) {
+        const size_t n = (size_t)c->src.n;
+        if (dbg->index) HIPCHK(hipMemcpyAsync(dbg->index, c->d_dbg_idx, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+        if (dbg->weight)
+            HIPCHK(hipMemcpyAsync(dbg->weight, c->d_dbg_w, sizeof(double) * n * d * d, hipMemcpyDeviceToHost, st));
+        if (dbg->distance)
+            HIPCHK(hipMemcpyAsync(dbg->distance, c->d_dbg_dist, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (c->timing) {
+        HIPCHK(hipEventElapsedTime(&c->last_corr_ms, c->ev[0], c->ev[1]));
+        HIPCHK(hipEventElapsedTime(&c->last_reduce_ms, c->ev[1], c->ev[2]));
+    }
+    const int ns = nstat(d);
+    c->last_amb = c->h_stats[ns];
+    c->last_pairs = c->h_stats[ns + 1];
+}
+
+}  // namespace
+
+namespace {
+int guard_impl(gicp_ctx* c, const char* where, const std::function<void()>& body) {
+    try {
+        if (c) HIPCHK(hipSetDevice(c->device));
+        body();
+        return GICP_OK;
+    } catch (const Fail& f) {
+        if (c) c->err = std::string(where) + ": " + f.msg;
+        return f.code;
+    } catch (const std::bad_alloc&) {
+        if (c) c->err = std::string(where) + ": out of host memory";
+        return GICP_E_NOMEM;
+    } catch (...) {
+        if (c) c->err = std::string(where) + ": unknown error";
+        return GICP_E_INVALID;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int gicp_version(void) { return 100; }
+
+int gicp_stats_size(int dim) { return (dim == 2 || dim == 3) ? nstat(dim == 2 ? 2 : 3) : GICP_E_INVALID; }
+
+void gicp_default_params(int dim, gicp_params* out) {
+    if (out) default_params(dim == 2 ? 2 : 3, out);
+}
+
+const char* gicp_strerror(int code) {
+    switch (code) {
+        case GICP_OK: return "ok";
+        case GICP_E_INVALID: return "invalid argument";
+        case GICP_E_HIP: return "HIP runtime error";
+        case GICP_E_STATE: return "call out of order";
+        case GICP_E_COMM: return "RCCL error";
+        case GICP_E_NOMEM: return "out of memory";
+        default: return "unknown error";
+    }
+}
+
+int gicp_create(gicp_ctx** out, int device) {
+    if (!out) return GICP_E_INVALID;
+    *out = nullptr;
+    gicp_ctx* c = new (std::nothrow) gicp_ctx();
+    if (!c) return GICP_E_NOMEM;
+    c->device = device;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        delete c;
+        return GICP_E_HIP;
+    }
+    if (device < 0 || device >= ndev) {
+        delete c;
+        return GICP_E_INVALID;
+    }
+    const int rc = guard_impl(c, "gicp_create", [&] {
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+        dalloc(c->d_amb, 4);
+        HIPCHK(hipMemsetAsync(c->d_amb, 0, sizeof(int32_t) * 4, c->stream));
+    });
+    if (rc != GICP_OK) {
+        gicp_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return GICP_OK;
+}
+
+void gicp_destroy(gicp_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->tgt.release();
+    c->src.release();
+    dfree(c->d_hint);
+    dfree(c->d_partials);
+    dfree(c->d_stats);
+    dfree(c->d_amb);
+    dfree(c->d_dbg_idx);
+    dfree(c->d_dbg_w);
+    dfree(c->d_dbg_dist);
+    if (c->h_stats) (void)hipHostFree(c->h_stats);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* gicp_last_error(const gicp_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int gicp_comm_unique_id(char out[GICP_COMM_ID_BYTES]) {
+    if (!out) return GICP_E_INVALID;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return GICP_E_COMM;
+    static_assert(sizeof(id) == GICP_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(out, &id, sizeof(id));
+    return GICP_OK;
+}
+
+int gicp_comm_init(gicp_ctx* c, int nranks, int rank, const char id[GICP_COMM_ID_BYTES]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_comm_init", [&] {
+        if (c->comm) {
+            ncclCommDestroy(c->comm);
+            c->comm = nullptr;
+        }
+        if (nranks == 1) return;
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof(uid));
+        ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+        if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+        c->nranks = nranks;
+        c->rank = rank;
+    });
+}
+
+int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_set_target", [&] {
+        c->ptgt = resolve(dim, p);
+        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, 0, 1, true);
+        if (c->src.n) HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * std::max(1, c->src.ntiles), c->stream));
+    });
+}
+
+int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gicp_params* p, int shard,
+                    int nshards) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_set_source", [&] {
+        if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
+        c->psrc = resolve(dim, p);
+        build_cloud(c, c->src, xyz, N, dim, c->psrc, shard, nshards, nshards == 1);
+        set_shard(c, shard, nshards);
+        HIPCHK(hipStreamSynchronize(c->stream));
+    });
+}
+
+int gicp_target_to_source(gicp_ctx* c, int shard, int nshards) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_target_to_source", [&] {
+        if (!c->tgt.n) throw Fail{GICP_E_STATE, "no target to promote"};
+        c->src.release();
+        c->src = c->tgt;
+        c->tgt = Cloud();  // ownership moved
+        c->psrc = c->ptgt;
+        set_shard(c, shard, nshards);
+        HIPCHK(hipStreamSynchronize(c->stream));
+    });
+}
+
+int gicp_get_covariances(gicp_ctx* c, int which, double* out) {
+    if (!c || !out || (which != 0 && which != 1)) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_get_covariances", [&] {
+        Cloud& cl = which == 0 ? c->tgt : c->src;
+        if (!cl.n || !cl.cov_ready) throw Fail{GICP_E_STATE, "cloud not set"};
+        const int d = cl.dim;
+        std::vector<double4> cv(cl.n);
+        std::vector<int32_t> perm(cl.n);
+        HIPCHK(hipMemcpyAsync(cv.data(), cl.cov, sizeof(double4) * cl.n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(perm.data(), cl.perm, sizeof(int32_t) * cl.n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int64_t i = 0; i < cl.n; ++i) {
+            const double m[3] = {cv[i].y, cv[i].z, cv[i].w};
+            double* o = out + (int64_t)perm[i] * d * d;
+            for (int a = 0; a < d; ++a)
+                for (int b = 0; b < d; ++b) o[a * d + b] = (a == b ? cv[i].x : 0.0) - m[a] * m[b];
+        }
+    });
+}
+
+int gicp_get_neighbor_counts(gicp_ctx* c, int which, int32_t* out) {
+    if (!c || !out || (which != 0 && which != 1)) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_get_neighbor_counts", [&] {
+        Cloud& cl = which == 0 ? c->tgt : c->src;
+        if (!cl.n) throw Fail{GICP_E_STATE, "cloud not set"};
+        std::vector<int32_t> cnt(cl.n), perm(cl.n);
+        HIPCHK(hipMemcpyAsync(cnt.data(), cl.ncount, sizeof(int32_t) * cl.n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(perm.data(), cl.perm, sizeof(int32_t) * cl.n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int64_t i = 0; i < cl.n; ++i) out[perm[i]] = cnt[i];
+    });
+}
+
+int gicp_iterate(gicp_ctx* c, const double* T, double* stats, gicp_debug* dbg) {
+    if (!c || !T || !stats) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_iterate", [&] {
+        run_pass(c, T, dbg);
+        std::memcpy(stats, c->h_stats, sizeof(double) * nstat(c->src.dim));
+    });
+}
+
+int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_out, double* loss_out) {
+    if ((dim != 2 && dim != 3) || !stats || !T_k || !T_out) return GICP_E_INVALID;
+    try {
+        return solve_pose(dim, stats, T_k, T_out, loss_out) == 0 ? GICP_OK : GICP_E_INVALID;
+    } catch (...) {
+        return GICP_E_INVALID;
+    }
+}
+
+int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_out, gicp_result* res) {
+    if (!c || !T_out) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_align", [&] {
+        if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
+        const int d = c->src.dim, n1 = d + 1;
+        gicp_params prm = p ? resolve(d, p) : c->psrc;
+        c->psrc.max_distance_correspondence = prm.max_distance_correspondence;
+        double T[16], Tn[16];
+        for (int k = 0; k < n1 * n1; ++k) T[k] = T0 ? T0[k] : ((k % (n1 + 1)) == 0 ? 1.0 : 0.0);
+        double last = INFINITY, loss = 0.0;
+        gicp_result r;
+        std::memset(&r, 0, sizeof(r));
+        r.converged_at = -1;
+        c->timing = res != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        double corr_ms = 0.0, red_ms = 0.0;
+        std::vector<double> st(nstat(d));
+        int it = 0;
+        for (; it < prm.max_iterations; ++it) {
+            run_pass(c, T, nullptr);
+            corr_ms += c->last_corr_ms;
+            red_ms += c->last_reduce_ms;
+            std::memcpy(st.data(), c->h_stats, sizeof(double) * st.size());
+            if (solve_pose(d, st.data(), T, Tn, &loss) != 0) throw Fail{GICP_E_INVALID, "pose solve failed"};
+            r.final_loss = loss;
+            r.correspondences = (int64_t)st[nstat(d) - 1];
+            if (!prm.fixed_iterations && std::fabs(last - loss) < prm.tolerance) {  // gicp.py:160-162
+                r.converged = 1;
+                r.converged_at = it;
+                ++it;
+                break;
+            }
+            last = loss;
+            std::memcpy(T, Tn, sizeof(double) * n1 * n1);
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        c->timing = false;
+        std::memcpy(T_out, T, sizeof(double) * n1 * n1);
+        r.iterations = it;
+        r.ambiguous = (int32_t)c->last_amb;
+        r.pairs_evaluated = (int64_t)c->last_pairs;
+        r.wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        r.corr_kernel_ms = corr_ms;
+        r.reduce_ms = red_ms;
+        if (res) *res = r;
+    });
+}
+
+}  // extern "C"

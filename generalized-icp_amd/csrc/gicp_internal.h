@@ -1,0 +1,95 @@
+// gicp_internal.h — device data layout shared by the HIP kernels and the host context.
+//
+// Every cloud (target and source) is stored Morton-sorted and cut into TILES of at most
+// 64 consecutive points that never cross a grid cell of the chosen Morton level, so a
+// tile is spatially compact (radius bounded by the cell).  64 consecutive tiles form a
+// BLOCK.  Both carry an fp64 centre and fp32 half-extents; points are kept twice:
+// fp64 (exact epilogue, fp64 fallback) and fp32 relative to their tile centre (the
+// distance screen).  See DESIGN.md §3.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gicp {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kTile = 64;          // points per tile (= one wave of queries)
+constexpr int kBlockTiles = 64;    // tiles per block (= one wave of tile tests)
+constexpr int kWavesPerWG = 4;     // 256-thread workgroups, each wave independent
+
+struct __attribute__((aligned(16))) TileInfo {
+    double c[3];      // fp64 centre (midpoint of the fp64 AABB)
+    float h[3];       // half-extents: max |rel32| over the tile's points, per axis
+    int32_t start;    // first sorted point
+    int32_t count;    // 1..64
+    float radius;     // max |rel32| norm
+};
+
+struct __attribute__((aligned(16))) BlockInfo {
+    double c[3];
+    float h[3];
+    int32_t first;    // first tile
+    int32_t ntiles;   // 1..64
+    float pad;
+};
+
+// Device view of one indexed cloud (all pointers device memory, sorted order).
+struct DevCloud {
+    const double* xyz64;      // [n][4]  x y z 0
+    const float4* rel32;      // [n]     x y z 0 relative to the tile centre
+    const double4* cov;       // [n]     (a, m0, m1, m2): C = a I - m m^T
+    const int32_t* perm;      // [n]     sorted -> original index
+    const TileInfo* tiles;    // [ntiles]
+    const BlockInfo* blocks;  // [nblocks]
+    const uint32_t* tile_code;// [ntiles] Morton code of each tile's first point
+    int64_t n;
+    int32_t ntiles;
+    int32_t nblocks;
+    double lo[3];             // Morton frame: code_a = (x_a - lo_a) * scale
+    double scale;
+    int32_t bits;             // bits per axis (10 for 3-D, 16 for 2-D)
+    int32_t dim;
+};
+
+// Error bound of the fp32 distance screen: |d2_f32 - d2_f64| <= a sqrt(d2) + b + c d2.
+struct Margin {
+    float a, b, c;
+};
+
+struct CovArgs {
+    DevCloud cl;
+    int32_t q_begin, q_end;   // query tiles
+    float search2;            // fp32 screen bound (d_n^2 + margins)
+    double dn2;               // d_n^2, fp64, strict
+    Margin mg;
+    double eps_a;             // epsilon (a of C = a I - m m^T)
+    double m_scale;           // sqrt(epsilon (1 - ratio))
+    int32_t min_nb;           // minimum neighbours for a surface covariance
+    double4* cov_out;         // [n] sorted
+    int32_t* count_out;       // [n] sorted
+    int32_t* amb_counter;     // diagnostics (may be null)
+};
+
+struct CorrArgs {
+    DevCloud src, tgt;
+    int32_t q_begin, q_end;   // this rank's source tiles
+    double R[9], t[3];
+    float R32[9];
+    float search2;            // fp32 screen bound (d_c^2 + margins)
+    double dc;                // d_c, fp64, inclusive (distance > d_c rejects)
+    Margin mg;
+    int32_t* hint;            // [src.ntiles] best target tile of the previous pass
+    double* partials;         // [gridDim.x][nstat_ext]
+    int64_t* dbg_index;       // [N] original order (nullable)
+    double* dbg_weight;       // [N][dim][dim] (nullable)
+    double* dbg_dist;         // [N] (nullable)
+    int32_t count_pairs;      // 1: accumulate evaluated pairs (diagnostic)
+};
+
+constexpr int nstat(int D) {
+    return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;
+}
+// partials carry two extra diagnostics: ambiguous count, pairs evaluated
+constexpr int nstat_ext(int D) { return nstat(D) + 2; }
+
+}  // namespace gicp

@@ -1,0 +1,936 @@
+// gicp_kernels.hip — the MI355X (gfx950) hot path of GICP.
+//
+// Reference behaviour (python-implementation/gicp.py):
+//   k_knn_cov   <- compute_covariance_matrix / _single_point, gicp.py:5-35
+//                  (k nearest incl. self, distance strictly < d_n, np.cov, eig ->
+//                  surface-aligned covariance; identity for isolated points)
+//   k_corr      <- the per-iteration correspondence + weight loop, gicp.py:119-145
+//                  (exact 1-NN in the target, accept d <= d_c, W = inv(C_s + C_t)),
+//                  fused with the sufficient statistics of loss()/grad_loss()
+//                  (gicp.py:52-76) so the inner minimisation needs no further pass
+//   k_reduce    <- deterministic sum of the per-workgroup statistics
+//
+// Design: one wave = one query tile of <= 64 Morton-coherent points.
+// Database tiles are culled with a two-level AABB hierarchy (blocks of 64 tiles, tested
+// one per lane, ballot), staged through LDS as fp32 SoA and scanned with a
+// broadcast read; lanes keep packed (d2 | row) keys.  The fp32 screen carries an
+// explicit error bound: a lane whose winner is within that bound of a rival (or of
+// the d_n / d_c cut) is re-resolved exactly in fp64, so indices match an fp64
+// KD-tree exactly.  No MFMA: there is no dense contraction in this path.
+#include <hip/hip_runtime.h>
+
+#include "gicp_internal.h"
+
+namespace gicp {
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
+    return max(min(a, b), min(max(a, b), c));
+}
+__device__ __forceinline__ float key_d2(unsigned k) { return __uint_as_float(k & ~63u); }
+__device__ __forceinline__ float marg(const Margin& m, float d2) { return fmaf(m.a, sqrtf(d2), fmaf(m.c, d2, m.b)); }
+
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_mind(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_maxd(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// exact-rounding fp64 square distance, summed in axis order without FMA contraction
+// (the order a KD-tree accumulates it in)
+template <int D>
+__device__ __forceinline__ double dist2_exact(const double* a, const double* b) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const double d = __dsub_rn(a[k], b[k]);
+        s = __dadd_rn(s, __dmul_rn(d, d));
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint32_t spread2(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+__device__ __forceinline__ uint32_t spread3(uint32_t x) {
+    x &= 0x3FFu;
+    x = (x | (x << 16)) & 0x030000FFu;
+    x = (x | (x << 8)) & 0x0300F00Fu;
+    x = (x | (x << 4)) & 0x030C30C3u;
+    x = (x | (x << 2)) & 0x09249249u;
+    return x;
+}
+__device__ __forceinline__ uint32_t morton_code(const double* p, int dim, const double* lo, double scale, int bits) {
+    const double maxc = (double)((1u << bits) - 1u);
+    uint32_t q[3] = {0, 0, 0};
+    for (int a = 0; a < dim; ++a) {
+        double v = (p[a] - lo[a]) * scale;
+        v = fmin(fmax(v, 0.0), maxc);
+        q[a] = (uint32_t)v;
+    }
+    return dim == 3 ? (spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2))
+                    : (spread2(q[0]) | (spread2(q[1]) << 1));
+}
+
+// ---------------------------------------------------------------------------
+// index build
+// ---------------------------------------------------------------------------
+__global__ void k_morton(const double* __restrict__ xyz, int64_t n, int dim, DevCloud fr, uint32_t* codes,
+                         int32_t* idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double p[3] = {0, 0, 0};
+    for (int a = 0; a < dim; ++a) p[a] = xyz[i * dim + a];
+    codes[i] = morton_code(p, dim, fr.lo, fr.scale, fr.bits);
+    idx[i] = (int32_t)i;
+}
+
+// One wave per tile: gather the tile's points (original order -> sorted), fp64 AABB,
+// centre, fp32 relative coordinates, half-extents and radius.
+__global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ xyz_in, int dim,
+                                                      const int32_t* __restrict__ perm, TileInfo* tiles, int ntiles,
+                                                      double* xyz64, float4* rel32, int32_t* inv,
+                                                      unsigned* rho_bits) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int T = blockIdx.x * kWavesPerWG + w;
+    if (T >= ntiles) return;
+    const int start = tiles[T].start, count = tiles[T].count;
+    const bool v = l < count;
+    const int i = start + l;
+    double p[3] = {0, 0, 0};
+    if (v) {
+        const int o = perm[i];
+        for (int a = 0; a < dim; ++a) p[a] = xyz_in[(int64_t)o * dim + a];
+        inv[o] = i;
+        double4 q;
+        q.x = p[0];
+        q.y = p[1];
+        q.z = p[2];
+        q.w = 0.0;
+        reinterpret_cast<double4*>(xyz64)[i] = q;
+    }
+    double c[3];
+    for (int a = 0; a < 3; ++a) {
+        const double mn = wave_mind(v ? p[a] : 1e300);
+        const double mx = wave_maxd(v ? p[a] : -1e300);
+        c[a] = a < dim ? 0.5 * (mn + mx) : 0.0;
+    }
+    float r[3];
+    for (int a = 0; a < 3; ++a) r[a] = v ? (float)(p[a] - c[a]) : 0.0f;
+    if (v) rel32[i] = make_float4(r[0], r[1], r[2], 0.0f);
+    float h[3];
+    for (int a = 0; a < 3; ++a) h[a] = wave_maxf(fabsf(r[a]));
+    const float rad = wave_maxf(sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]));
+    if (l == 0) {
+        TileInfo& t = tiles[T];
+        for (int a = 0; a < 3; ++a) {
+            t.c[a] = c[a];
+            t.h[a] = h[a];
+        }
+        t.radius = rad;
+        atomicMax(rho_bits, __float_as_uint(rad));
+    }
+}
+
+// One wave per block of 64 tiles: fp64 AABB over the tiles' boxes.
+__global__ void __launch_bounds__(256) k_build_blocks(const TileInfo* __restrict__ tiles, int ntiles, BlockInfo* blocks,
+                                                       int nblocks, int dim) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int B = blockIdx.x * kWavesPerWG + w;
+    if (B >= nblocks) return;
+    const int t = B * kBlockTiles + l;
+    const bool v = t < ntiles;
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = v ? tiles[t].c[a] - (double)tiles[t].h[a] : 1e300;
+        hi[a] = v ? tiles[t].c[a] + (double)tiles[t].h[a] : -1e300;
+        lo[a] = wave_mind(lo[a]);
+        hi[a] = wave_maxd(hi[a]);
+    }
+    if (l == 0) {
+        BlockInfo& b = blocks[B];
+        for (int a = 0; a < 3; ++a) {
+            const double c = a < dim ? 0.5 * (lo[a] + hi[a]) : 0.0;
+            const double hh = a < dim ? 0.5 * (hi[a] - lo[a]) : 0.0;
+            b.c[a] = c;
+            b.h[a] = __double2float_ru(hh) * (1.0f + 1e-6f);
+        }
+        b.first = B * kBlockTiles;
+        b.ntiles = min(kBlockTiles, ntiles - B * kBlockTiles);
+        b.pad = 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// traversal
+// ---------------------------------------------------------------------------
+template <int D>
+struct Query {
+    double ow[D];   // wave origin (query tile centre, transformed), uniform
+    float ew[D];    // half-extents of the query tile around ow, uniform, conservative
+    float pw[D];    // lane point relative to ow, fp32
+    double p64[D];  // lane point, fp64 (transformed)
+    bool valid;
+};
+
+// squared gap between the wave box (ow +- ew) and a box (c +- h); conservative in fp32
+template <int D>
+__device__ __forceinline__ float gap2_box(const Query<D>& q, const double* c, const float* h) {
+    float g2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const float dl = fabsf((float)(q.ow[a] - c[a]));
+        float g = dl - q.ew[a] - h[a];
+        g -= (dl + q.ew[a] + h[a]) * 9.5367431640625e-7f;  // 2^-20 slack
+        g = fmaxf(g, 0.f);
+        g2 = fmaf(g, g, g2);
+    }
+    return g2;
+}
+
+// Two-level culled walk over the database tiles.  `visit(T)` returns true when it
+// processed the tile (the wave's bound then shrinks); `wave_bound()` is the max over
+// lanes of the squared search radius still needed.
+template <int D, class Visit, class WB>
+__device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, int seed, Visit&& visit,
+                                         WB&& wave_bound) {
+    const int l = lane_id();
+    float wb = wave_bound();
+    if (seed >= 0) {
+        if (visit(seed)) wb = wave_bound();
+    }
+    for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
+        const int b = b0 + l;
+        bool cb = false;
+        if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wb;
+        uint64_t bm = __ballot(cb);
+        while (bm) {
+            const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
+            bm &= bm - 1;
+            const int first = db.blocks[bb].first, nt = db.blocks[bb].ntiles;
+            const int t = first + l;
+            bool ct = false;
+            if (l < nt && t != seed) ct = gap2_box<D>(q, db.tiles[t].c, db.tiles[t].h) <= wb;
+            uint64_t tm = __ballot(ct);
+            while (tm) {
+                const int T = first + __ffsll((unsigned long long)tm) - 1;
+                tm &= tm - 1;
+                if (visit(T)) wb = wave_bound();
+            }
+        }
+    }
+}
+
+// per-wave LDS staging area
+struct WaveLds {
+    float x[kTile], y[kTile], z[kTile];
+    double x64[kTile], y64[kTile], z64[kTile];
+};
+
+// Lane point relative to database tile T, and the per-lane squared gap to T's box.
+template <int D>
+__device__ __forceinline__ float lane_gap2(const Query<D>& q, const TileInfo& ti, float* pr) {
+    float g2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        pr[a] = q.pw[a] + (float)(q.ow[a] - ti.c[a]);
+        const float ap = fabsf(pr[a]);
+        float g = ap - ti.h[a] - (ap + ti.h[a]) * 9.5367431640625e-7f;
+        g = fmaxf(g, 0.f);
+        g2 = fmaf(g, g, g2);
+    }
+    return g2;
+}
+
+// stage a tile's fp32 coordinates (padding rows at 1e30: their distance is +inf)
+__device__ __forceinline__ void stage_f32(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
+    const int l = lane_id();
+    float4 v = make_float4(1e30f, 1e30f, 1e30f, 0.f);
+    if (l < ti.count) v = db.rel32[ti.start + l];
+    L.x[l] = v.x;
+    L.y[l] = v.y;
+    L.z[l] = v.z;
+    wave_sync();
+}
+__device__ __forceinline__ void stage_f64(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
+    const int l = lane_id();
+    double4 v;
+    v.x = v.y = v.z = 1e150;
+    v.w = 0.0;
+    if (l < ti.count) v = reinterpret_cast<const double4*>(db.xyz64)[ti.start + l];
+    L.x64[l] = v.x;
+    L.y64[l] = v.y;
+    L.z64[l] = v.z;
+    wave_sync();
+}
+
+template <int D>
+__device__ __forceinline__ unsigned row_key(const float* pr, float qx, float qy, float qz, int j) {
+    const float dx = pr[0] - qx;
+    const float dy = pr[1] - qy;
+    float d2 = fmaf(dy, dy, dx * dx);
+    if (D == 3) {
+        const float dz = pr[2] - qz;
+        d2 = fmaf(dz, dz, d2);
+    }
+    return (__float_as_uint(d2) & ~63u) | (unsigned)j;
+}
+
+// Scan one staged tile: calls row(key) for every row (4 rows per LDS read group).
+template <int D, class Row>
+__device__ __forceinline__ void scan_tile(const WaveLds& L, int count, const float* pr, Row&& row) {
+    const int n4 = (count + 3) & ~3;
+    for (int j = 0; j < n4; j += 4) {
+        const float4 X = *reinterpret_cast<const float4*>(L.x + j);
+        const float4 Y = *reinterpret_cast<const float4*>(L.y + j);
+        float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (D == 3) Z = *reinterpret_cast<const float4*>(L.z + j);
+        row(row_key<D>(pr, X.x, Y.x, Z.x, j), j);
+        row(row_key<D>(pr, X.y, Y.y, Z.y, j + 1), j + 1);
+        row(row_key<D>(pr, X.z, Y.z, Z.z, j + 2), j + 2);
+        row(row_key<D>(pr, X.w, Y.w, Z.w, j + 3), j + 3);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// surface covariance: k nearest (self included, < d_n), shifted sums, eigen
+// ---------------------------------------------------------------------------
+template <int D>
+struct CovSums {
+    double n;
+    double s[D];
+    double ss[D * (D + 1) / 2];
+};
+
+template <int D>
+__device__ __forceinline__ void cov_add(CovSums<D>& A, const double* d) {
+    A.n += 1.0;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        A.s[a] += d[a];
+#pragma unroll
+        for (int b = a; b < D; ++b) A.ss[k++] += d[a] * d[b];
+    }
+}
+
+// Symmetric 3x3 eigenvector of the smallest eigenvalue (cyclic Jacobi, fp64).
+__device__ __forceinline__ void smallest_eigvec3(double A[3][3], double* n) {
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        const double off = fabs(A[0][1]) + fabs(A[0][2]) + fabs(A[1][2]);
+        if (off == 0.0) break;
+#pragma unroll
+        for (int pq = 0; pq < 3; ++pq) {
+            const int p = pq == 2 ? 1 : 0;
+            const int qq = pq == 0 ? 1 : 2;
+            const double apq = A[p][qq];
+            if (apq == 0.0) continue;
+            const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
+            const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+            for (int k = 0; k < 3; ++k) {  // A <- J^T A J
+                const double akp = A[k][p], akq = A[k][qq];
+                A[k][p] = c * akp - s * akq;
+                A[k][qq] = s * akp + c * akq;
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double apk = A[p][k], aqk = A[qq][k];
+                A[p][k] = c * apk - s * aqk;
+                A[qq][k] = s * apk + c * aqk;
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double vkp = V[k][p], vkq = V[k][qq];
+                V[k][p] = c * vkp - s * vkq;
+                V[k][qq] = s * vkp + c * vkq;
+            }
+        }
+    }
+    int m = 0;
+    if (A[1][1] < A[m][m]) m = 1;
+    if (A[2][2] < A[m][m]) m = 2;
+    for (int k = 0; k < 3; ++k) n[k] = V[k][m];
+}
+
+// C = a I - m m^T from the neighbourhood sums (gicp.py:11-16 / SURVEY.md §8.A)
+template <int D>
+__device__ __forceinline__ double4 cov_descriptor(const CovSums<D>& A, int min_nb, double eps_a, double m_scale) {
+    double4 out;
+    out.x = 1.0;
+    out.y = out.z = out.w = 0.0;  // identity (gicp.py:33-34)
+    if (A.n < (double)min_nb) return out;
+    const double n = A.n;
+    double C[D][D];
+    int k = 0;
+    for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) {
+            C[a][b] = C[b][a] = (A.ss[k] - A.s[a] * A.s[b] / n) / (n - 1.0);
+            ++k;
+        }
+    out.x = eps_a;
+    if (D == 2) {
+        // principal eigenvector at 0.5 atan2(2 cxy, cxx - cyy); thin direction is its normal
+        const double phi = 0.5 * atan2(2.0 * C[0][1], C[0][0] - C[1][1]);
+        double sp, cp;
+        sincos(phi, &sp, &cp);
+        out.y = -sp * m_scale;
+        out.z = cp * m_scale;
+    } else {
+        double M[3][3];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) M[a][b] = C[a % D][b % D];
+        double nv[3];
+        smallest_eigvec3(M, nv);
+        out.y = nv[0] * m_scale;
+        out.z = nv[1] * m_scale;
+        out.w = nv[2] * m_scale;
+    }
+    return out;
+}
+
+template <int D, int K>
+__global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
+    __shared__ WaveLds s_lds[kWavesPerWG];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int T = A.q_begin + blockIdx.x * kWavesPerWG + w;
+    if (T >= A.q_end) return;  // waves are independent (no workgroup barrier here)
+    WaveLds& L = s_lds[w];
+    const DevCloud& cl = A.cl;
+    const TileInfo qt = cl.tiles[T];
+
+    Query<D> q;
+    q.valid = l < qt.count;
+    const int i = qt.start + min(l, qt.count - 1);
+    const float4 rel = cl.rel32[i];
+    const double4 p4 = reinterpret_cast<const double4*>(cl.xyz64)[i];
+    const float relv[3] = {rel.x, rel.y, rel.z};
+    const double p4v[3] = {p4.x, p4.y, p4.z};
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        q.ow[a] = qt.c[a];
+        q.ew[a] = qt.h[a];
+        q.pw[a] = relv[a];
+        q.p64[a] = p4v[a];
+    }
+
+    // ---- phase 1: fp32 screen for the K+1 smallest keys ------------------
+    constexpr int K1 = K + 1;
+    const unsigned init = __float_as_uint(A.search2) | 63u;
+    unsigned lk[K1];
+#pragma unroll
+    for (int m = 0; m < K1; ++m) lk[m] = init;
+    auto lane_bound = [&]() -> float {
+        if (!q.valid) return -1.f;
+        const float kk = key_d2(lk[K1 - 1]), km = key_d2(lk[K1 - 2]);
+        return fminf(kk, km + 2.f * marg(A.mg, km));
+    };
+    auto visit1 = [&](int Tt) -> bool {
+        const TileInfo& ti = cl.tiles[Tt];
+        float pr[D];
+        const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
+        if (!__any(need)) return false;
+        stage_f32(cl, ti, L);
+        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
+            if (__any(key < lk[K1 - 1])) {
+#pragma unroll
+                for (int m = K1 - 1; m > 0; --m) lk[m] = umed3(lk[m - 1], lk[m], key);
+                lk[0] = min(lk[0], key);
+            }
+        });
+        wave_sync();
+        return true;
+    };
+    traverse<D>(cl, q, T, visit1, [&]() { return wave_maxf(lane_bound()); });
+
+    int c = 0;
+#pragma unroll
+    for (int m = 0; m < K1; ++m) c += lk[m] < init ? 1 : 0;
+    const int nacc = min(c, K);
+    unsigned tau = init;
+#pragma unroll
+    for (int m = 0; m < K; ++m)
+        if (m == nacc - 1) tau = lk[m];
+    const float tau_d2 = key_d2(tau);
+    bool amb = false;
+    if (c > K) {
+        const float a1 = key_d2(lk[K - 1]), a2 = key_d2(lk[K]);
+        amb = (a2 - a1) <= marg(A.mg, a1) + marg(A.mg, a2);
+    }
+    const float dn2_lo = (float)A.dn2 * (1.0f - 2.4e-7f);
+    if (tau_d2 + marg(A.mg, tau_d2) >= dn2_lo) amb = true;
+    amb = amb && q.valid;
+
+    // ---- phase 2: fp64 shifted sums over the accepted keys ------------------
+    CovSums<D> S;
+    S.n = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) S.s[a] = 0.0;
+#pragma unroll
+    for (int k = 0; k < D * (D + 1) / 2; ++k) S.ss[k] = 0.0;
+    const bool take_lane = q.valid && !amb;
+    // cull by the top of tau's truncation bucket: a point keyed <= tau may screen above key_d2(tau)
+    const float tau_hi = __uint_as_float((tau | 63u) + 1u);
+    auto visit2 = [&](int Tt) -> bool {
+        const TileInfo& ti = cl.tiles[Tt];
+        float pr[D];
+        const bool need = take_lane && lane_gap2<D>(q, ti, pr) <= tau_hi;
+        if (!__any(need)) return false;
+        stage_f32(cl, ti, L);
+        stage_f64(cl, ti, L);
+        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int j) {
+            const bool take = take_lane && key <= tau;
+            if (__any(take)) {
+                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                double d[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) d[a] = qq[a] - q.p64[a];
+                if (take) cov_add<D>(S, d);
+            }
+        });
+        wave_sync();
+        return true;
+    };
+    traverse<D>(cl, q, T, visit2, [&]() { return wave_maxf(take_lane ? tau_hi : -1.f); });
+
+    // ---- fp64 fallback for lanes the screen could not decide ----------------
+    if (__any(amb)) {
+        if (A.amb_counter && l == 0) atomicAdd(A.amb_counter, __popcll(__ballot(amb)));
+        double lk64[K];
+#pragma unroll
+        for (int m = 0; m < K; ++m) lk64[m] = A.dn2;
+        const float bound_f = A.search2;
+        auto visit3 = [&](int Tt) -> bool {
+            const TileInfo& ti = cl.tiles[Tt];
+            float pr[D];
+            const float b64 = (float)lk64[K - 1];
+            const bool need = amb && lane_gap2<D>(q, ti, pr) <= b64 + 2.f * marg(A.mg, b64);
+            if (!__any(need)) return false;
+            stage_f64(cl, ti, L);
+            for (int j = 0; j < ti.count; ++j) {
+                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                const double d2 = dist2_exact<D>(qq, q.p64);
+                if (__any(amb && d2 < lk64[K - 1])) {
+                    if (amb) {
+#pragma unroll
+                        for (int m = K - 1; m > 0; --m) lk64[m] = fmin(lk64[m], fmax(lk64[m - 1], d2));
+                        lk64[0] = fmin(lk64[0], d2);
+                    }
+                }
+            }
+            wave_sync();
+            return true;
+        };
+        traverse<D>(cl, q, T, visit3, [&]() { return wave_maxf(amb ? bound_f : -1.f); });
+        int c64 = 0;
+#pragma unroll
+        for (int m = 0; m < K; ++m) c64 += lk64[m] < A.dn2 ? 1 : 0;
+        double tau64 = A.dn2;
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+            if (m == c64 - 1) tau64 = lk64[m];
+        int nless = 0;
+#pragma unroll
+        for (int m = 0; m < K; ++m) nless += lk64[m] < tau64 ? 1 : 0;
+        int eq_left = c64 - nless;
+        auto visit4 = [&](int Tt) -> bool {
+            const TileInfo& ti = cl.tiles[Tt];
+            float pr[D];
+            const float b64 = (float)tau64;
+            const bool need = amb && lane_gap2<D>(q, ti, pr) <= b64 + 2.f * marg(A.mg, b64);
+            if (!__any(need)) return false;
+            stage_f64(cl, ti, L);
+            for (int j = 0; j < ti.count; ++j) {
+                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                const double d2 = dist2_exact<D>(qq, q.p64);
+                bool take = amb && c64 > 0 && (d2 < tau64 || (d2 == tau64 && eq_left > 0));
+                if (take && d2 == tau64) --eq_left;
+                if (__any(take)) {
+                    double d[D];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) d[a] = qq[a] - q.p64[a];
+                    if (take) cov_add<D>(S, d);
+                }
+            }
+            wave_sync();
+            return true;
+        };
+        traverse<D>(cl, q, T, visit4, [&]() {
+            const float b64 = (float)tau64;
+            return wave_maxf(amb ? b64 + 2.f * marg(A.mg, b64) : -1.f);
+        });
+    }
+
+    if (q.valid) {
+        A.cov_out[i] = cov_descriptor<D>(S, A.min_nb, A.eps_a, A.m_scale);
+        A.count_out[i] = (int)S.n;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-iteration correspondences + weights + statistics
+// ---------------------------------------------------------------------------
+template <int D>
+struct StatIdx {
+    static constexpr int NS = D * (D + 1) / 2;
+    static constexpr int pa(int p) { return D == 3 ? (p < 3 ? 0 : (p < 5 ? 1 : 2)) : (p < 2 ? 0 : 1); }
+    static constexpr int pb(int p) {
+        return D == 3 ? (p == 0 ? 0 : p == 1 ? 1 : p == 2 ? 2 : p == 3 ? 1 : 2) : (p == 0 ? 0 : 1);
+    }
+};
+
+// statistic k of one point: A[ab][ij], B[ab][i], C[ab], gR[a][i], gt[a], c0, count
+template <int D>
+__device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], const double (&s)[D],
+                                             const double (&wr)[D], double rwr) {
+    using SI = StatIdx<D>;
+    constexpr int NS = SI::NS;
+    if (k < NS * NS) {
+        const int p = k / NS, qd = k % NS;
+        return W[SI::pa(p)][SI::pb(p)] * (s[SI::pa(qd)] * s[SI::pb(qd)]);
+    }
+    k -= NS * NS;
+    if (k < NS * D) return W[SI::pa(k / D)][SI::pb(k / D)] * s[k % D];
+    k -= NS * D;
+    if (k < NS) return W[SI::pa(k)][SI::pb(k)];
+    k -= NS;
+    if (k < D * D) return wr[k / D] * s[k % D];
+    k -= D * D;
+    if (k < D) return wr[k];
+    k -= D;
+    if (k == 0) return rwr;
+    return 1.0;
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
+    constexpr int NSX = nstat_ext(D);
+    constexpr int NSS = nstat(D);
+    constexpr int CH = 8, CHS = 72;  // 8 statistics per chunk, row stride 72 doubles (bank-conflict free)
+    __shared__ WaveLds s_lds[kWavesPerWG];
+    __shared__ double s_chunk[kWavesPerWG][CH * CHS];
+    __shared__ double s_wstat[kWavesPerWG][NSX];
+
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int T = A.q_begin + blockIdx.x * kWavesPerWG + w;
+    const bool active = T < A.q_end;
+    WaveLds& L = s_lds[w];
+    const DevCloud& sc = A.src;
+    const DevCloud& tg = A.tgt;
+
+    bool on = false;          // accepted correspondence
+    double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0;
+    bool amb = false;
+    int pairs = 0;
+
+    if (active) {
+        const TileInfo st = sc.tiles[T];
+        Query<D> q;
+        q.valid = l < st.count;
+        const int i = st.start + min(l, st.count - 1);
+        const float4 rel = sc.rel32[i];
+        const double4 s4 = reinterpret_cast<const double4*>(sc.xyz64)[i];
+        const float relv[3] = {rel.x, rel.y, rel.z};
+        const double s4v[3] = {s4.x, s4.y, s4.z};
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            double o = A.t[a], p = A.t[a];
+            float pw = 0.f, ew = 0.f;
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                o += A.R[a * D + b] * st.c[b];
+                p += A.R[a * D + b] * s4v[b];
+                pw = fmaf(A.R32[a * D + b], relv[b], pw);
+                ew = fmaf(fabsf(A.R32[a * D + b]), st.h[b], ew);
+            }
+            q.ow[a] = o;
+            q.p64[a] = p;
+            q.pw[a] = pw;
+            q.ew[a] = ew * (1.0f + 4.8e-7f) + 1e-30f;
+            sv[a] = s4v[a];
+        }
+
+        // seed: last pass's best target tile for this source tile, else the Morton neighbour
+        int seed = A.hint ? A.hint[T] : -1;
+        if (seed < 0 || seed >= tg.ntiles) {
+            const uint32_t code = morton_code(q.ow, D, tg.lo, tg.scale, tg.bits);
+            int lo = 0, hi = tg.ntiles - 1;
+            while (lo < hi) {  // last tile whose first code <= code
+                const int mid = (lo + hi + 1) >> 1;
+                if (tg.tile_code[mid] <= code) lo = mid;
+                else hi = mid - 1;
+            }
+            seed = lo;
+        }
+
+        // ---- fp32 screen: best and runner-up keys -------------------------
+        const unsigned init = __float_as_uint(A.search2) | 63u;
+        unsigned best = init, sec = init;
+        int best_tile = -1;
+        auto lane_bound = [&]() -> float {
+            if (!q.valid) return -1.f;
+            const float b = key_d2(best);
+            return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
+        };
+        auto visit = [&](int Tt) -> bool {
+            const TileInfo& ti = tg.tiles[Tt];
+            float pr[D];
+            const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
+            if (!__any(need)) return false;
+            stage_f32(tg, ti, L);
+            unsigned tb = 0xFFFFFFFFu, ts = 0xFFFFFFFFu;
+            scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
+                ts = umed3(tb, ts, key);
+                tb = min(tb, key);
+            });
+            if (tb < best) {
+                sec = min(best, ts);
+                best = tb;
+                best_tile = Tt;
+            } else {
+                sec = min(sec, tb);
+            }
+            pairs += ti.count;
+            wave_sync();
+            return true;
+        };
+        traverse<D>(tg, q, seed, visit, [&]() { return wave_maxf(lane_bound()); });
+
+        const bool found = q.valid && best < init;
+        int j = -1;
+        double d2e = 0.0;
+        if (found) {
+            const float b = key_d2(best), s2 = key_d2(sec);
+            amb = (s2 - b) <= marg(A.mg, b) + marg(A.mg, s2);
+            j = tg.tiles[best_tile].start + (int)(best & 63u);
+        }
+        // hint for the next pass: the first lane's winning tile
+        const uint64_t fm = __ballot(found);
+        if (fm && A.hint) {
+            const int src_lane = __ffsll((unsigned long long)fm) - 1;
+            const int bt = __shfl(best_tile, src_lane);
+            if (l == 0) A.hint[T] = bt;
+        }
+
+        // ---- fp64 re-resolution of the lanes the screen could not decide ----
+        if (__any(amb)) {
+            double bd2 = 1e300;
+            int bj = -1, bo = 0x7FFFFFFF;
+            const float lim = key_d2(best) + 2.f * marg(A.mg, key_d2(best));
+            auto visit64 = [&](int Tt) -> bool {
+                const TileInfo& ti = tg.tiles[Tt];
+                float pr[D];
+                const bool need = amb && lane_gap2<D>(q, ti, pr) <= lim;
+                if (!__any(need)) return false;
+                stage_f64(tg, ti, L);
+                for (int jj = 0; jj < ti.count; ++jj) {
+                    const double qq[3] = {L.x64[jj], L.y64[jj], L.z64[jj]};
+                    const double d2 = dist2_exact<D>(qq, q.p64);
+                    const int gj = ti.start + jj;
+                    const int og = tg.perm[gj];
+                    if (amb && (d2 < bd2 || (d2 == bd2 && og < bo))) {
+                        bd2 = d2;
+                        bj = gj;
+                        bo = og;
+                    }
+                }
+                wave_sync();
+                return true;
+            };
+            traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
+            if (amb) j = bj;
+        }
+
+        // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
+        if (found && j >= 0) {
+            const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
+            const double qv[3] = {q4.x, q4.y, q4.z};
+            d2e = dist2_exact<D>(qv, q.p64);
+            const double dist = sqrt(d2e);
+            if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = dist;
+            if (!(dist > A.dc)) {  // gicp.py:136: reject only if distance > d_c
+                on = true;
+                const double4 cs = sc.cov[i];
+                const double4 ct = tg.cov[j];
+                const double ms[3] = {cs.y, cs.z, cs.w};
+                const double mt[3] = {ct.y, ct.z, ct.w};
+                double mr[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    mr[a] = 0.0;
+#pragma unroll
+                    for (int b = 0; b < D; ++b) mr[a] += A.R[a * D + b] * ms[b];
+                }
+                double S[D][D];
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+#pragma unroll
+                    for (int b = 0; b < D; ++b)
+                        S[a][b] = (a == b ? cs.x + ct.x : 0.0) - mr[a] * mr[b] - mt[a] * mt[b];
+                if (D == 2) {
+                    const double det = S[0][0] * S[1][1] - S[0][1] * S[1][0];
+                    W[0][0] = S[1][1] / det;
+                    W[1][1] = S[0][0] / det;
+                    W[0][1] = W[1][0] = -S[0][1] / det;
+                } else {
+                    const double c00 = S[1][1] * S[2][2] - S[1][2] * S[2][1];
+                    const double c01 = S[0][2] * S[2][1] - S[0][1] * S[2][2];
+                    const double c02 = S[0][1] * S[1][2] - S[0][2] * S[1][1];
+                    const double c11 = S[0][0] * S[2][2] - S[0][2] * S[2][0];
+                    const double c12 = S[0][2] * S[1][0] - S[0][0] * S[1][2];
+                    const double c22 = S[0][0] * S[1][1] - S[0][1] * S[1][0];
+                    const double det = S[0][0] * c00 + S[0][1] * c01 + S[0][2] * c02;
+                    const double id = 1.0 / det;
+                    W[0][0] = c00 * id;
+                    W[0][1] = W[1][0] = c01 * id;
+                    W[0][2] = W[2][0] = c02 * id;
+                    W[1][1] = c11 * id;
+                    W[1][2] = W[2][1] = c12 * id;
+                    W[2][2] = c22 * id;
+                }
+                double r[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) r[a] = qv[a] - q.p64[a];
+                rwr = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    wr[a] = 0.0;
+#pragma unroll
+                    for (int b = 0; b < D; ++b) wr[a] += W[a][b] * r[b];
+                    rwr += r[a] * wr[a];
+                }
+            }
+            if (A.dbg_index) A.dbg_index[sc.perm[i]] = on ? (int64_t)tg.perm[j] : -1;
+        } else if (q.valid) {
+            if (A.dbg_index) A.dbg_index[sc.perm[i]] = -1;
+            if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = 1.0 / 0.0;
+        }
+        if (A.dbg_weight && q.valid) {
+            double* o = A.dbg_weight + (int64_t)sc.perm[i] * D * D;
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int b = 0; b < D; ++b) o[a * D + b] = on ? W[a][b] : 0.0;
+        }
+        amb = amb && q.valid;
+    }
+
+    // ---- wave reduction of the statistics: 8 at a time through LDS ------------
+    double* ch = s_chunk[w];
+#pragma unroll
+    for (int c0 = 0; c0 < NSX; c0 += CH) {
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int idx = c0 + k;
+            if (idx < NSS) ch[k * CHS + l] = on ? stat_value<D>(idx, W, sv, wr, rwr) : 0.0;
+            else if (idx == NSS) ch[k * CHS + l] = amb ? 1.0 : 0.0;
+            else if (idx == NSS + 1) ch[k * CHS + l] = l == 0 ? (double)pairs * 64.0 : 0.0;
+        }
+        wave_sync();
+        const int k = l >> 3, part = l & 7;
+        double sum = 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += ch[k * CHS + u * 8 + part];
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        sum += __shfl_xor(sum, 4);
+        if (part == 0 && c0 + k < NSX) s_wstat[w][c0 + k] = sum;
+        wave_sync();
+    }
+    __syncthreads();
+    if (threadIdx.x < NSX) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < kWavesPerWG; ++u) s += s_wstat[u][threadIdx.x];
+        A.partials[(int64_t)blockIdx.x * NSX + threadIdx.x] = s;
+    }
+}
+
+// Deterministic sum of the per-workgroup partials: one workgroup per statistic.
+__global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ partials, int nparts, int nsx,
+                                                 double* __restrict__ out) {
+    __shared__ double sh[256];
+    const int v = blockIdx.x;
+    double s = 0.0;
+    for (int p = threadIdx.x; p < nparts; p += 256) s += partials[(int64_t)p * nsx + v];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[v] = sh[0];
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& fr, uint32_t* codes, int32_t* idx,
+                         hipStream_t st) {
+    const int bs = 256;
+    const unsigned g = (unsigned)((n + bs - 1) / bs);
+    hipLaunchKernelGGL(k_morton, dim3(g), dim3(bs), 0, st, xyz, n, dim, fr, codes, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_tiles(const double* xyz_in, int dim, const int32_t* perm, TileInfo* tiles, int ntiles,
+                              double* xyz64, float4* rel32, int32_t* inv, unsigned* rho_bits, hipStream_t st) {
+    const unsigned g = (unsigned)((ntiles + kWavesPerWG - 1) / kWavesPerWG);
+    hipLaunchKernelGGL(k_build_tiles, dim3(g), dim3(256), 0, st, xyz_in, dim, perm, tiles, ntiles, xyz64, rel32, inv,
+                       rho_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blocks, int nblocks, int dim,
+                               hipStream_t st) {
+    const unsigned g = (unsigned)((nblocks + kWavesPerWG - 1) / kWavesPerWG);
+    hipLaunchKernelGGL(k_build_blocks, dim3(g), dim3(256), 0, st, tiles, ntiles, blocks, nblocks, dim);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
+    const int nq = a.q_end - a.q_begin;
+    if (nq <= 0) return hipSuccess;
+    const unsigned g = (unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG);
+    if (dim == 2 && k == 6) hipLaunchKernelGGL((k_knn_cov<2, 6>), dim3(g), dim3(256), 0, st, a);
+    else if (dim == 3 && k == 20) hipLaunchKernelGGL((k_knn_cov<3, 20>), dim3(g), dim3(256), 0, st, a);
+    else if (dim == 3 && k == 10) hipLaunchKernelGGL((k_knn_cov<3, 10>), dim3(g), dim3(256), 0, st, a);
+    else if (dim == 2 && k == 10) hipLaunchKernelGGL((k_knn_cov<2, 10>), dim3(g), dim3(256), 0, st, a);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+int corr_grid(int q_tiles) { return (q_tiles + kWavesPerWG - 1) / kWavesPerWG; }
+
+hipError_t launch_corr(const CorrArgs& a, int dim, hipStream_t st) {
+    const int g = corr_grid(a.q_end - a.q_begin);
+    if (g <= 0) return hipSuccess;
+    if (dim == 2) hipLaunchKernelGGL(k_corr<2>, dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_corr<3>, dim3(g), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double* partials, int nparts, int nsx, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce, dim3(nsx), dim3(256), 0, st, partials, nparts, nsx, out);
+    return hipGetLastError();
+}
+
+}  // namespace gicp

@@ -1,0 +1,311 @@
+"""MI355X-native GICP — drop-in for msi-se/generalized-icp's ``gicp.py``.
+
+``from gicp import gicp, apply_transformation`` works as with the reference
+(python-implementation/gicp.py:78, :176; imported that way by
+visualization.py:7 and robot-visualization.py:6).  The per-iteration hot path
+(correspondences, Mahalanobis weights, normal-equation statistics) and the
+per-point surface covariances run in hand-written HIP kernels for gfx950
+behind the C-ABI of ``libgicp_hip.so``; this module is the thin host layer.
+
+There is no CPU fallback: without the built library or a GPU the engine
+raises.  HIP is initialised on the first call, not at import (the reference
+calls gicp() from a forked worker, robot-visualization.py:199).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import Debug, Params, Result, check, dptr
+
+__all__ = ["gicp", "apply_transformation", "Engine", "expand_stats", "stats_size", "default_params"]
+
+
+def stats_size(dim):
+    ns = dim * (dim + 1) // 2
+    return ns * ns + ns * dim + ns + dim * dim + dim + 2
+
+
+def default_params(dim, **kw):
+    """gicp_params with the reference defaults (gicp.py:5, :11, :24, :78), overridden by kw."""
+    p = Params()
+    _lib.load().gicp_default_params(dim, C.byref(p))
+    for k, v in kw.items():
+        if v is not None:
+            setattr(p, k, v)
+    return p
+
+
+def _sym_pairs(d):
+    return [(a, b) for a in range(d) for b in range(a, d)]
+
+
+def expand_stats(st, d):
+    """(H, g, c0, count) of  f(z) = c0 - 2 g.(z - z_k) + (z - z_k)^T H (z - z_k),  z = (vec R, t).
+
+    Layout of ``st``: A[ab][ij] = sum W_ab s_i s_j, B[ab][i] = sum W_ab s_i,
+    C[ab] = sum W_ab, gR[a][i] = sum (W r_k)_a s_i, gt[a] = sum (W r_k)_a, c0, count."""
+    st = np.asarray(st, dtype=np.float64)
+    P = _sym_pairs(d)
+    ns = len(P)
+    pos = {}
+    for k, (a, b) in enumerate(P):
+        pos[(a, b)] = pos[(b, a)] = k
+    o = 0
+    A = st[o:o + ns * ns].reshape(ns, ns); o += ns * ns
+    B = st[o:o + ns * d].reshape(ns, d); o += ns * d
+    Cc = st[o:o + ns]; o += ns
+    gR = st[o:o + d * d].reshape(d, d); o += d * d
+    gt = st[o:o + d]; o += d
+    nz = d * d + d
+    H = np.zeros((nz, nz))
+    for a in range(d):
+        for i in range(d):
+            for b in range(d):
+                for j in range(d):
+                    H[a * d + i, b * d + j] = A[pos[(a, b)], pos[(i, j)]]
+                H[a * d + i, d * d + b] = H[d * d + b, a * d + i] = B[pos[(a, b)], i]
+        for b in range(d):
+            H[d * d + a, d * d + b] = Cc[pos[(a, b)]]
+    return H, np.concatenate([gR.ravel(), gt]), float(st[o]), float(st[o + 1])
+
+
+# 2-D: z6 = (R00, R01, R10, R11, tx, ty) = L (tx, ty, cos th, sin th)
+_L2 = np.array([[0, 0, 1, 0], [0, 0, 0, -1], [0, 0, 0, 1], [0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0]], dtype=np.float64)
+
+
+def _rot2(theta):
+    c, s = np.cos(theta), np.sin(theta)
+    return np.array([[c, -s], [s, c]])
+
+
+def _offset_to_T(x):
+    """gicp.py:42-50."""
+    T = np.eye(3)
+    T[:2, :2] = _rot2(x[2])
+    T[:2, 2] = x[:2]
+    return T
+
+
+def apply_transformation(cloud, T):
+    """gicp.py:176-177 (any dimension: x -> R x + t)."""
+    T = np.asarray(T)
+    d = T.shape[0] - 1
+    return np.dot(np.asarray(cloud)[:, :d], T[:d, :d].T) + T[:d, d]
+
+
+class Engine:
+    """One GPU context of libgicp_hip.so (clouds stay resident between calls)."""
+
+    def __init__(self, device=0):
+        self._lib = _lib.load()
+        self._ctx = C.c_void_p()
+        rc = self._lib.gicp_create(C.byref(self._ctx), int(device))
+        if rc != _lib.GICP_OK:
+            raise _lib.GicpError(rc, f"gicp_create(device={device}): {self._lib.gicp_strerror(rc).decode()}")
+        self.device = device
+        self.dim = None
+        self.n_src = self.n_tgt = 0
+
+    def close(self):
+        if self._ctx:
+            self._lib.gicp_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _cloud(pts):
+        a = np.ascontiguousarray(np.asarray(pts, dtype=np.float64))
+        if a.ndim != 2 or a.shape[1] not in (2, 3) or a.shape[0] < 1:
+            raise ValueError(f"point cloud must be a non-empty N x 2 or N x 3 array, got shape {a.shape}")
+        return a
+
+    def comm_init(self, nranks, rank, uid: bytes):
+        check(self._lib.gicp_comm_init(self._ctx, nranks, rank, uid), self._ctx, "gicp_comm_init")
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(_lib.COMM_ID_BYTES)
+        check(_lib.load().gicp_comm_unique_id(buf), None, "gicp_comm_unique_id")
+        return buf.raw
+
+    def set_target(self, pts, params=None):
+        a = self._cloud(pts)
+        p = params or default_params(a.shape[1])
+        check(self._lib.gicp_set_target(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p)), self._ctx,
+              "gicp_set_target")
+        self.n_tgt, self.dim = a.shape
+
+    def set_source(self, pts, params=None, shard=0, nshards=1):
+        a = self._cloud(pts)
+        p = params or default_params(a.shape[1])
+        check(self._lib.gicp_set_source(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p), shard, nshards),
+              self._ctx, "gicp_set_source")
+        self.n_src, self.dim = a.shape
+
+    def target_to_source(self, shard=0, nshards=1):
+        check(self._lib.gicp_target_to_source(self._ctx, shard, nshards), self._ctx, "gicp_target_to_source")
+        self.n_src = self.n_tgt
+        self.n_tgt = 0
+
+    def covariances(self, which="target"):
+        w = 0 if which == "target" else 1
+        n = self.n_tgt if w == 0 else self.n_src
+        out = np.empty((n, self.dim, self.dim))
+        check(self._lib.gicp_get_covariances(self._ctx, w, dptr(out)), self._ctx, "gicp_get_covariances")
+        return out
+
+    def neighbor_counts(self, which="target"):
+        w = 0 if which == "target" else 1
+        n = self.n_tgt if w == 0 else self.n_src
+        out = np.empty(n, dtype=np.int32)
+        check(self._lib.gicp_get_neighbor_counts(self._ctx, w, out.ctypes.data_as(C.POINTER(C.c_int32))), self._ctx,
+              "gicp_get_neighbor_counts")
+        return out
+
+    def iterate(self, T, debug=False):
+        """One pass at pose T -> statistics (and per-point index / W / distance if debug)."""
+        T = np.ascontiguousarray(np.asarray(T, dtype=np.float64))
+        st = np.empty(stats_size(self.dim))
+        dbg = None
+        out = None
+        if debug:
+            n, d = self.n_src, self.dim
+            out = dict(index=np.empty(n, dtype=np.int64), weight=np.empty((n, d, d)), distance=np.empty(n))
+            dbg = Debug(out["index"].ctypes.data_as(C.POINTER(C.c_int64)), dptr(out["weight"]), dptr(out["distance"]))
+        check(self._lib.gicp_iterate(self._ctx, dptr(T), dptr(st), C.byref(dbg) if dbg else None), self._ctx,
+              "gicp_iterate")
+        return (st, out) if debug else st
+
+    def align(self, T0=None, params=None):
+        """The whole outer loop (gicp.py:116-167) natively; returns (T, result dict)."""
+        d = self.dim
+        T0 = np.eye(d + 1) if T0 is None else np.ascontiguousarray(np.asarray(T0, dtype=np.float64))
+        Tout = np.empty((d + 1, d + 1))
+        res = Result()
+        p = params or default_params(d)
+        check(self._lib.gicp_align(self._ctx, dptr(T0), C.byref(p), dptr(Tout), C.byref(res)), self._ctx,
+              "gicp_align")
+        return Tout, res.as_dict()
+
+
+def solve_pose(stats, T_k):
+    """Host minimiser of the inner problem from the statistics (gicp_solve_pose)."""
+    T_k = np.ascontiguousarray(np.asarray(T_k, dtype=np.float64))
+    d = T_k.shape[0] - 1
+    st = np.ascontiguousarray(np.asarray(stats, dtype=np.float64))
+    out = np.empty_like(T_k)
+    loss = C.c_double()
+    check(_lib.load().gicp_solve_pose(d, dptr(st), dptr(T_k), dptr(out), C.byref(loss)), None, "gicp_solve_pose")
+    return out, loss.value
+
+
+def _cg_inner(stats, offset, T_k):
+    """2-D reference inner solve: scipy fmin_cg on the closed-form loss (gicp.py:148-154)."""
+    from scipy.optimize import fmin_cg
+
+    H6, g6, c0, _ = expand_stats(stats, 2)
+    H4 = _L2.T @ H6 @ _L2
+    g4 = _L2.T @ g6
+    th = np.arctan2(T_k[1, 0], T_k[0, 0])
+    zk = np.array([T_k[0, 2], T_k[1, 2], T_k[0, 0], T_k[1, 0]])
+
+    def z(x):
+        return np.array([x[0], x[1], np.cos(x[2]), np.sin(x[2])])
+
+    def f(x):
+        dz = z(x) - zk
+        return c0 - 2.0 * g4 @ dz + dz @ H4 @ dz
+
+    def g(x):
+        dz = z(x) - zk
+        v = -2.0 * g4 + 2.0 * (H4 @ dz)
+        return np.array([v[0], v[1], -np.sin(x[2]) * v[2] + np.cos(x[2]) * v[3]])
+
+    del th
+    out = fmin_cg(f=f, x0=offset, fprime=g, disp=False, full_output=True)
+    return out[0], out[1]
+
+
+_ENGINES = {}
+
+
+def _engine(device):
+    eng = _ENGINES.get(device)
+    if eng is None:
+        eng = _ENGINES[device] = Engine(device)
+    return eng
+
+
+def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
+         max_distance_nearest_neighbors=50, *, full_output=True, inner=None, k_neighbors=None, device=0,
+         verbose=True, T0=None):
+    """Drop-in for gicp.py:78 — returns the same 7-tuple (gicp.py:174):
+
+    (T, all_transformations, initial_source_cov_matrices, target_cov_matrices,
+     highest_weight_points_source, highest_weight_points_target, all_source_cov_matrices)
+
+    2-D and 3-D clouds (T is 3x3 or 4x4).  ``inner``: 'cg' (2-D default:
+    scipy fmin_cg on the GPU-reduced closed form, reproducing the reference's
+    inexact inner stop) or 'newton' (exact minimiser on SO(d); 3-D default).
+    ``full_output=False`` skips the per-point visualisation extras (the lists
+    come back empty), which is what large clouds want.
+    """
+    src = Engine._cloud(source_points)
+    tgt = Engine._cloud(target_points)
+    d = src.shape[1]
+    if tgt.shape[1] != d:
+        raise ValueError("source and target must have the same dimension")
+    inner = ("cg" if d == 2 else "newton") if inner is None else inner
+    if inner not in ("cg", "newton") or (inner == "cg" and d != 2):
+        raise ValueError("inner must be 'newton', or 'cg' for 2-D clouds")
+    eng = _engine(device)
+    p = default_params(d, max_iterations=int(max_iterations), tolerance=float(tolerance),
+                       max_distance_correspondence=float(max_distance_correspondence),
+                       max_distance_nearest_neighbors=float(max_distance_nearest_neighbors), k_neighbors=k_neighbors)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    target_cov = eng.covariances("target")
+    init_src_cov = eng.covariances("source")
+    T = np.eye(d + 1) if T0 is None else np.array(T0, dtype=np.float64)
+    all_T = [T]
+    offset = np.array([T[0, 2], T[1, 2], np.arctan2(T[1, 0], T[0, 0])]) if d == 2 else None
+    last = np.inf
+    hw_s, hw_t, all_src_cov = [], [], []
+    for it in range(int(max_iterations)):
+        if full_output:
+            st, dbg = eng.iterate(T, debug=True)
+            R = T[:d, :d]
+            all_src_cov.append(np.einsum("ab,nbc,dc->nad", R, init_src_cov, R))
+        else:
+            st = eng.iterate(T)
+        if inner == "cg":
+            new_offset, min_loss = _cg_inner(st, offset, T)
+            T_new = _offset_to_T(new_offset)
+        else:
+            T_new, min_loss = solve_pose(st, T)
+            new_offset = None
+        if abs(last - min_loss) < tolerance:                       # gicp.py:155-162
+            if verbose:
+                print("Converged at iteration", it)
+            break
+        last = min_loss
+        if full_output:                                            # gicp.py:169-172
+            moved = apply_transformation(src, T)
+            idx = dbg["index"]
+            q = np.zeros_like(src)
+            q[idx >= 0] = tgt[idx[idx >= 0]]
+            top = np.argsort(np.linalg.det(dbg["weight"]))[-5:]
+            hw_s.append(moved[top])
+            hw_t.append(q[top])
+        offset = new_offset
+        T = T_new
+        all_T.append(T)
+    return T, all_T, init_src_cov, target_cov, hw_s, hw_t, all_src_cov

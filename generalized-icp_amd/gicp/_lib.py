@@ -1,0 +1,125 @@
+"""ctypes binding of libgicp_hip.so (include/gicp_hip.h).
+
+The shared library is built in-tree (``make -C generalized-icp_amd/csrc`` or
+``__graft_entry__.build()``) and loaded from this directory.  There is no CPU
+fallback: if the library is missing the import of the engine fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgicp_hip.so")
+
+GICP_OK = 0
+GICP_E_INVALID = -1
+GICP_E_HIP = -2
+GICP_E_STATE = -3
+GICP_E_COMM = -4
+GICP_E_NOMEM = -5
+COMM_ID_BYTES = 128
+
+
+class Params(C.Structure):
+    """gicp_params (include/gicp_hip.h) — gicp.py:78 keyword arguments + its constants."""
+    _fields_ = [
+        ("max_iterations", C.c_int32),
+        ("k_neighbors", C.c_int32),
+        ("tolerance", C.c_double),
+        ("max_distance_correspondence", C.c_double),
+        ("max_distance_nearest_neighbors", C.c_double),
+        ("epsilon", C.c_double),
+        ("ratio", C.c_double),
+        ("fixed_iterations", C.c_int32),
+        ("min_neighbors", C.c_int32),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int32),
+        ("converged", C.c_int32),
+        ("converged_at", C.c_int32),
+        ("ambiguous", C.c_int32),
+        ("final_loss", C.c_double),
+        ("correspondences", C.c_int64),
+        ("wall_ms", C.c_double),
+        ("corr_kernel_ms", C.c_double),
+        ("reduce_ms", C.c_double),
+        ("pairs_evaluated", C.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Debug(C.Structure):
+    _fields_ = [
+        ("index", C.POINTER(C.c_int64)),
+        ("weight", C.POINTER(C.c_double)),
+        ("distance", C.POINTER(C.c_double)),
+    ]
+
+
+# every entry point include/gicp_hip.h declares: name -> (restype, argtypes)
+_VP = C.c_void_p
+_DP = C.POINTER(C.c_double)
+SIGNATURES = {
+    "gicp_version": (C.c_int, []),
+    "gicp_stats_size": (C.c_int, [C.c_int]),
+    "gicp_default_params": (None, [C.c_int, C.POINTER(Params)]),
+    "gicp_strerror": (C.c_char_p, [C.c_int]),
+    "gicp_create": (C.c_int, [C.POINTER(_VP), C.c_int]),
+    "gicp_destroy": (None, [_VP]),
+    "gicp_last_error": (C.c_char_p, [_VP]),
+    "gicp_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "gicp_comm_init": (C.c_int, [_VP, C.c_int, C.c_int, C.c_char_p]),
+    "gicp_set_target": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params)]),
+    "gicp_set_source": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params), C.c_int, C.c_int]),
+    "gicp_target_to_source": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "gicp_get_covariances": (C.c_int, [_VP, C.c_int, _DP]),
+    "gicp_get_neighbor_counts": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int32)]),
+    "gicp_iterate": (C.c_int, [_VP, _DP, _DP, C.POINTER(Debug)]),
+    "gicp_solve_pose": (C.c_int, [C.c_int, _DP, _DP, _DP, _DP]),
+    "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libgicp_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libgicp_hip.so not found at {LIB_PATH}; build it with "
+                          "`make -C generalized-icp_amd/csrc` (there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class GicpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def check(rc, ctx=None, what=""):
+    if rc == GICP_OK:
+        return
+    lib = load()
+    msg = lib.gicp_last_error(ctx).decode() if ctx else lib.gicp_strerror(rc).decode()
+    if rc == GICP_E_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise GicpError(rc, f"{what}: {msg}")
+
+
+def dptr(a):
+    return a.ctypes.data_as(_DP)

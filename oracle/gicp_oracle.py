@@ -37,12 +37,12 @@ def default_k(dim):
 # ---------------------------------------------------------------------------
 # covariances: gicp.py:5-35
 # ---------------------------------------------------------------------------
-def neighbourhoods(points, d_n, k=None):
+def neighbourhoods(points, d_n, k=None, workers=1):
     """k nearest (self included) with distance strictly < d_n — gicp.py:21-25."""
     pts = np.asarray(points, dtype=np.float64)
     k = default_k(pts.shape[1]) if k is None else k
     tree = cKDTree(pts)
-    dist, idx = tree.query(pts, k=min(k, len(pts)), distance_upper_bound=d_n)
+    dist, idx = tree.query(pts, k=min(k, len(pts)), distance_upper_bound=d_n, workers=workers)
     if idx.ndim == 1:
         dist, idx = dist[:, None], idx[:, None]
     valid = idx < len(pts)                      # gicp.py:25 drops index == len(points)
@@ -59,7 +59,7 @@ def covariance_single_2d(neigh, epsilon=EPSILON, ratio=RATIO):
     return rv @ ground @ rv.T
 
 
-def covariances(points, d_n, k=None, epsilon=EPSILON, ratio=RATIO, min_neighbors=None, faithful=None):
+def covariances(points, d_n, k=None, epsilon=EPSILON, ratio=RATIO, min_neighbors=None, faithful=None, workers=1):
     """Per-point surface covariances (gicp.py:19-35).
 
     2-D: > 1 neighbour -> ``covariance_single_2d`` else identity (gicp.py:27-34).
@@ -73,7 +73,7 @@ def covariances(points, d_n, k=None, epsilon=EPSILON, ratio=RATIO, min_neighbors
     pts = np.asarray(points, dtype=np.float64)
     n, dim = pts.shape
     min_neighbors = (2 if dim == 2 else 3) if min_neighbors is None else min_neighbors
-    idx, valid, _ = neighbourhoods(pts, d_n, k)
+    idx, valid, _ = neighbourhoods(pts, d_n, k, workers)
     count = valid.sum(axis=1)
     out = np.empty((n, dim, dim))
     out[:] = np.eye(dim)
@@ -113,10 +113,10 @@ def apply_transformation(cloud, T):
     return np.dot(np.asarray(cloud)[:, :d], T[:d, :d].T) + T[:d, d]
 
 
-def correspondences(points, target, d_c, tree=None):
+def correspondences(points, target, d_c, tree=None, workers=1):
     """Exact 1-NN in the target (gicp.py:127-133); accepted if d <= d_c (gicp.py:136)."""
     tree = cKDTree(target) if tree is None else tree
-    dist, idx = tree.query(points, k=1)
+    dist, idx = tree.query(points, k=1, workers=workers)
     ok = dist <= d_c
     return np.where(ok, idx, -1), dist
 
