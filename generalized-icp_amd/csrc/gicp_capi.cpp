@@ -410,6 +410,17 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     const int nsx = nstat_ext(d);
     const int grid = corr_grid(c->q_end - c->q_begin);
     hipStream_t st = c->stream;
+#ifdef GICP_STAMPS
+    static unsigned long long* d_stamps = nullptr;
+    static size_t stamps_cap = 0;
+    const size_t nst = (size_t)std::max(1, grid) * kWavesPerWG * 8;
+    if (nst > stamps_cap) {
+        dalloc(d_stamps, nst);
+        stamps_cap = nst;
+    }
+    HIPCHK(hipMemsetAsync(d_stamps, 0, nst * 8, st));
+    a.stamps = d_stamps;
+#endif
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], st));
     if (grid > 0) HIPCHK(launch_corr(a, d, st));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], st));
@@ -434,6 +445,28 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
         HIPCHK(hipEventElapsedTime(&c->last_corr_ms, c->ev[0], c->ev[1]));
         HIPCHK(hipEventElapsedTime(&c->last_reduce_ms, c->ev[1], c->ev[2]));
     }
+#ifdef GICP_STAMPS
+    {
+        std::vector<unsigned long long> hs(nst);
+        HIPCHK(hipMemcpy(hs.data(), d_stamps, nst * 8, hipMemcpyDeviceToHost));
+        double tot[8] = {0}, all = 0;
+        int nw = 0;
+        for (size_t w = 0; w < nst / 8; ++w) {
+            unsigned long long r = 0;
+            for (int k = 0; k < 8; ++k) r += hs[w * 8 + k];
+            if (!r) continue;
+            ++nw;
+            for (int k = 0; k < 8; ++k) {
+                tot[k] += (double)hs[w * 8 + k];
+                all += (double)hs[w * 8 + k];
+            }
+        }
+        static const char* nm[8] = {"setup", "traverse", "need+stage", "scan", "fallback", "epilogue", "reduce", "-"};
+        std::fprintf(stderr, "[stamps] waves %d, mean cycles/wave %.0f:", nw, all / std::max(1, nw));
+        for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * tot[k] / std::max(1.0, all));
+        std::fprintf(stderr, "\n");
+    }
+#endif
     const int ns = nstat(d);
     c->last_amb = c->h_stats[ns];
     c->last_pairs = c->h_stats[ns + 1];

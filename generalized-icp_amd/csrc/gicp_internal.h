@@ -84,6 +84,7 @@ struct CorrArgs {
     double* dbg_weight;       // [N][dim][dim] (nullable)
     double* dbg_dist;         // [N] (nullable)
     int32_t count_pairs;      // 1: accumulate evaluated pairs (diagnostic)
+    unsigned long long* stamps;  // [waves][8] phase cycles (STAMPS diagnostic build only; else null)
 };
 
 constexpr int nstat(int D) {

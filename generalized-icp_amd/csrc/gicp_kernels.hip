@@ -19,6 +19,8 @@
 // KD-tree exactly.  No MFMA: there is no dense contraction in this path.
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "gicp_internal.h"
 
 namespace gicp {
@@ -33,10 +35,16 @@ __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
 __device__ __forceinline__ float key_d2(unsigned k) { return __uint_as_float(k & ~63u); }
 __device__ __forceinline__ float marg(const Margin& m, float d2) { return fmaf(m.a, sqrtf(d2), fmaf(m.c, d2, m.b)); }
 
+// wave-wide max, result uniform (SGPR): DPP row_shr 1/2/4/8, row_bcast 15/31, readlane 63
 __device__ __forceinline__ float wave_maxf(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    int x = __float_as_int(v);
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false))));
+    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false))));
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
 __device__ __forceinline__ double wave_mind(double v) {
 #pragma unroll
@@ -49,6 +57,25 @@ __device__ __forceinline__ double wave_maxd(double v) {
     return v;
 }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// Diagnostic-only phase timer (build with `make STAMPS=1`): s_memtime cycles per phase per wave.
+// 0 setup, 1 traversal tests, 2 tile need-test + staging, 3 row scan, 4 fp64 fallback,
+// 5 epilogue (W, statistics), 6 statistics reduction.  Compiles to nothing otherwise.
+struct Stamps {
+#ifdef GICP_STAMPS
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = 0;
+    __device__ __forceinline__ void start() { last = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void mark(int c) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[c] += t - last;
+        last = t;
+    }
+#else
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+#endif
+};
 
 // exact-rounding fp64 square distance, summed in axis order without FMA contraction
 // (the order a KD-tree accumulates it in)
@@ -240,10 +267,16 @@ __device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, 
     }
 }
 
-// per-wave LDS staging area
-struct WaveLds {
-    float x[kTile], y[kTile], z[kTile];
-    double x64[kTile], y64[kTile], z64[kTile];
+// per-wave LDS: tile staging during the walk, statistics transpose afterwards (same bytes)
+constexpr int kStatCh = 4;        // statistics per reduction round
+constexpr int kStatStride = 80;   // doubles per statistic row: conflict-free for the 16-lane reads
+struct WaveStage {
+    float x[kTile], y[kTile], z[kTile];           // fp32 screen coordinates, SoA
+    double x64[kTile], y64[kTile], z64[kTile];    // fp64 coordinates (covariance sums, fallback)
+};
+union __attribute__((aligned(16))) WaveLds {
+    WaveStage t;
+    double chunk[kStatCh * kStatStride];
 };
 
 // Lane point relative to database tile T, and the per-lane squared gap to T's box.
@@ -261,14 +294,19 @@ __device__ __forceinline__ float lane_gap2(const Query<D>& q, const TileInfo& ti
     return g2;
 }
 
+// uniform (scalar-cache) copy of a tile's metadata
+__device__ __forceinline__ TileInfo tile_meta(const DevCloud& db, int T) {
+    return db.tiles[__builtin_amdgcn_readfirstlane(T)];
+}
+
 // stage a tile's fp32 coordinates (padding rows at 1e30: their distance is +inf)
 __device__ __forceinline__ void stage_f32(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
     const int l = lane_id();
     float4 v = make_float4(1e30f, 1e30f, 1e30f, 0.f);
     if (l < ti.count) v = db.rel32[ti.start + l];
-    L.x[l] = v.x;
-    L.y[l] = v.y;
-    L.z[l] = v.z;
+    L.t.x[l] = v.x;
+    L.t.y[l] = v.y;
+    L.t.z[l] = v.z;
     wave_sync();
 }
 __device__ __forceinline__ void stage_f64(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
@@ -277,38 +315,62 @@ __device__ __forceinline__ void stage_f64(const DevCloud& db, const TileInfo& ti
     v.x = v.y = v.z = 1e150;
     v.w = 0.0;
     if (l < ti.count) v = reinterpret_cast<const double4*>(db.xyz64)[ti.start + l];
-    L.x64[l] = v.x;
-    L.y64[l] = v.y;
-    L.z64[l] = v.z;
+    L.t.x64[l] = v.x;
+    L.t.y64[l] = v.y;
+    L.t.z64[l] = v.z;
     wave_sync();
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// squared screen distance of the lane point to two database rows at once (v_pk_* fp32);
+// bit-identical to fmaf(dz, dz, fmaf(dy, dy, dx * dx)) per row
 template <int D>
-__device__ __forceinline__ unsigned row_key(const float* pr, float qx, float qy, float qz, int j) {
-    const float dx = pr[0] - qx;
-    const float dy = pr[1] - qy;
-    float d2 = fmaf(dy, dy, dx * dx);
+__device__ __forceinline__ f2v pair_d2(const float* pr, f2v qx, f2v qy, f2v qz) {
+    const f2v dx = f2v{pr[0], pr[0]} - qx;
+    const f2v dy = f2v{pr[1], pr[1]} - qy;
+    f2v d2 = __builtin_elementwise_fma(dy, dy, dx * dx);
     if (D == 3) {
-        const float dz = pr[2] - qz;
-        d2 = fmaf(dz, dz, d2);
+        const f2v dz = f2v{pr[2], pr[2]} - qz;
+        d2 = __builtin_elementwise_fma(dz, dz, d2);
     }
-    return (__float_as_uint(d2) & ~63u) | (unsigned)j;
+    return d2;
 }
 
-// Scan one staged tile: calls row(key) for every row (4 rows per LDS read group).
+// 0xFFFFFFC0 held in a VGPR so (d2 & mask) | row is one v_and_or_b32 (row stays an SGPR)
+__device__ __forceinline__ unsigned key_mask() {
+    unsigned m;
+    asm volatile("v_mov_b32 %0, 0xffffffc0" : "=v"(m));
+    return m;
+}
+
+// One group of 4 rows at compile-time offset J: 3 ds_read_b128 (SoA x/y/z), 2 packed pairs.
+template <int J, int D, class Row>
+__device__ __forceinline__ void scan_group(const WaveLds& L, const float* pr, unsigned M, Row& row) {
+    const float4 X = *reinterpret_cast<const float4*>(L.t.x + J);
+    const float4 Y = *reinterpret_cast<const float4*>(L.t.y + J);
+    float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (D == 3) Z = *reinterpret_cast<const float4*>(L.t.z + J);
+    const f2v a = pair_d2<D>(pr, f2v{X.x, X.y}, f2v{Y.x, Y.y}, f2v{Z.x, Z.y});
+    const f2v b = pair_d2<D>(pr, f2v{X.z, X.w}, f2v{Y.z, Y.w}, f2v{Z.z, Z.w});
+    row((__float_as_uint(a.x) & M) | (unsigned)J, J);
+    row((__float_as_uint(a.y) & M) | (unsigned)(J + 1), J + 1);
+    row((__float_as_uint(b.x) & M) | (unsigned)(J + 2), J + 2);
+    row((__float_as_uint(b.y) & M) | (unsigned)(J + 3), J + 3);
+}
+
+template <int D, class Row, int... G>
+__device__ __forceinline__ void scan_groups(const WaveLds& L, int n4, const float* pr, unsigned M, Row& row,
+                                            std::integer_sequence<int, G...>) {
+    // short-circuit fold: group G runs only while 4G < n4 (wave-uniform branch)
+    (void)((4 * G < n4 ? (scan_group<4 * G, D>(L, pr, M, row), true) : false) && ...);
+}
+
+// Scan one staged tile: row(key, j) for every row; key = (d2 bits & ~63) | row.
 template <int D, class Row>
 __device__ __forceinline__ void scan_tile(const WaveLds& L, int count, const float* pr, Row&& row) {
-    const int n4 = (count + 3) & ~3;
-    for (int j = 0; j < n4; j += 4) {
-        const float4 X = *reinterpret_cast<const float4*>(L.x + j);
-        const float4 Y = *reinterpret_cast<const float4*>(L.y + j);
-        float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (D == 3) Z = *reinterpret_cast<const float4*>(L.z + j);
-        row(row_key<D>(pr, X.x, Y.x, Z.x, j), j);
-        row(row_key<D>(pr, X.y, Y.y, Z.y, j + 1), j + 1);
-        row(row_key<D>(pr, X.z, Y.z, Z.z, j + 2), j + 2);
-        row(row_key<D>(pr, X.w, Y.w, Z.w, j + 3), j + 3);
-    }
+    const unsigned M = key_mask();
+    scan_groups<D>(L, (count + 3) & ~3, pr, M, row, std::make_integer_sequence<int, kTile / 4>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -444,7 +506,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         return fminf(kk, km + 2.f * marg(A.mg, km));
     };
     auto visit1 = [&](int Tt) -> bool {
-        const TileInfo& ti = cl.tiles[Tt];
+        const TileInfo ti = tile_meta(cl, Tt);
         float pr[D];
         const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
         if (!__any(need)) return false;
@@ -490,7 +552,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
     // cull by the top of tau's truncation bucket: a point keyed <= tau may screen above key_d2(tau)
     const float tau_hi = __uint_as_float((tau | 63u) + 1u);
     auto visit2 = [&](int Tt) -> bool {
-        const TileInfo& ti = cl.tiles[Tt];
+        const TileInfo ti = tile_meta(cl, Tt);
         float pr[D];
         const bool need = take_lane && lane_gap2<D>(q, ti, pr) <= tau_hi;
         if (!__any(need)) return false;
@@ -499,7 +561,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         scan_tile<D>(L, ti.count, pr, [&](unsigned key, int j) {
             const bool take = take_lane && key <= tau;
             if (__any(take)) {
-                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
                 double d[D];
 #pragma unroll
                 for (int a = 0; a < D; ++a) d[a] = qq[a] - q.p64[a];
@@ -519,14 +581,14 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         for (int m = 0; m < K; ++m) lk64[m] = A.dn2;
         const float bound_f = A.search2;
         auto visit3 = [&](int Tt) -> bool {
-            const TileInfo& ti = cl.tiles[Tt];
+            const TileInfo ti = tile_meta(cl, Tt);
             float pr[D];
             const float b64 = (float)lk64[K - 1];
             const bool need = amb && lane_gap2<D>(q, ti, pr) <= b64 + 2.f * marg(A.mg, b64);
             if (!__any(need)) return false;
             stage_f64(cl, ti, L);
             for (int j = 0; j < ti.count; ++j) {
-                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
                 const double d2 = dist2_exact<D>(qq, q.p64);
                 if (__any(amb && d2 < lk64[K - 1])) {
                     if (amb) {
@@ -552,14 +614,14 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         for (int m = 0; m < K; ++m) nless += lk64[m] < tau64 ? 1 : 0;
         int eq_left = c64 - nless;
         auto visit4 = [&](int Tt) -> bool {
-            const TileInfo& ti = cl.tiles[Tt];
+            const TileInfo ti = tile_meta(cl, Tt);
             float pr[D];
             const float b64 = (float)tau64;
             const bool need = amb && lane_gap2<D>(q, ti, pr) <= b64 + 2.f * marg(A.mg, b64);
             if (!__any(need)) return false;
             stage_f64(cl, ti, L);
             for (int j = 0; j < ti.count; ++j) {
-                const double qq[3] = {L.x64[j], L.y64[j], L.z64[j]};
+                const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
                 const double d2 = dist2_exact<D>(qq, q.p64);
                 bool take = amb && c64 > 0 && (d2 < tau64 || (d2 == tau64 && eq_left > 0));
                 if (take && d2 == tau64) --eq_left;
@@ -624,9 +686,7 @@ template <int D>
 __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
     constexpr int NSS = nstat(D);
-    constexpr int CH = 8, CHS = 72;  // 8 statistics per chunk, row stride 72 doubles (bank-conflict free)
     __shared__ WaveLds s_lds[kWavesPerWG];
-    __shared__ double s_chunk[kWavesPerWG][CH * CHS];
     __shared__ double s_wstat[kWavesPerWG][NSX];
 
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -636,6 +696,8 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
     const DevCloud& sc = A.src;
     const DevCloud& tg = A.tgt;
 
+    Stamps S;
+    S.start();
     bool on = false;          // accepted correspondence
     double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0;
     bool amb = false;
@@ -691,11 +753,16 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
         };
         auto visit = [&](int Tt) -> bool {
-            const TileInfo& ti = tg.tiles[Tt];
+            S.mark(1);
+            const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
             const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
-            if (!__any(need)) return false;
+            if (!__any(need)) {
+                S.mark(2);
+                return false;
+            }
             stage_f32(tg, ti, L);
+            S.mark(2);
             unsigned tb = 0xFFFFFFFFu, ts = 0xFFFFFFFFu;
             scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
                 ts = umed3(tb, ts, key);
@@ -710,9 +777,12 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             }
             pairs += ti.count;
             wave_sync();
+            S.mark(3);
             return true;
         };
+        S.mark(0);
         traverse<D>(tg, q, seed, visit, [&]() { return wave_maxf(lane_bound()); });
+        S.mark(1);
 
         const bool found = q.valid && best < init;
         int j = -1;
@@ -736,13 +806,13 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             int bj = -1, bo = 0x7FFFFFFF;
             const float lim = key_d2(best) + 2.f * marg(A.mg, key_d2(best));
             auto visit64 = [&](int Tt) -> bool {
-                const TileInfo& ti = tg.tiles[Tt];
+                const TileInfo ti = tile_meta(tg, Tt);
                 float pr[D];
                 const bool need = amb && lane_gap2<D>(q, ti, pr) <= lim;
                 if (!__any(need)) return false;
                 stage_f64(tg, ti, L);
                 for (int jj = 0; jj < ti.count; ++jj) {
-                    const double qq[3] = {L.x64[jj], L.y64[jj], L.z64[jj]};
+                    const double qq[3] = {L.t.x64[jj], L.t.y64[jj], L.t.z64[jj]};
                     const double d2 = dist2_exact<D>(qq, q.p64);
                     const int gj = ti.start + jj;
                     const int og = tg.perm[gj];
@@ -759,6 +829,7 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             if (amb) j = bj;
         }
 
+        S.mark(4);
         // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
         if (found && j >= 0) {
             const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
@@ -833,44 +904,55 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
         amb = amb && q.valid;
     }
 
-    // ---- wave reduction of the statistics: 8 at a time through LDS ------------
-    double* ch = s_chunk[w];
+    S.mark(5);
+    // ---- wave reduction of the statistics: 4 at a time through LDS (reusing the stage bytes)
+    wave_sync();
+    double* ch = s_lds[w].chunk;
 #pragma unroll
-    for (int c0 = 0; c0 < NSX; c0 += CH) {
+    for (int c0 = 0; c0 < NSX; c0 += kStatCh) {
 #pragma unroll
-        for (int k = 0; k < CH; ++k) {
+        for (int k = 0; k < kStatCh; ++k) {
             const int idx = c0 + k;
-            if (idx < NSS) ch[k * CHS + l] = on ? stat_value<D>(idx, W, sv, wr, rwr) : 0.0;
-            else if (idx == NSS) ch[k * CHS + l] = amb ? 1.0 : 0.0;
-            else if (idx == NSS + 1) ch[k * CHS + l] = l == 0 ? (double)pairs * 64.0 : 0.0;
+            double v = 0.0;
+            if (idx < NSS) v = on ? stat_value<D>(idx, W, sv, wr, rwr) : 0.0;
+            else if (idx == NSS) v = amb ? 1.0 : 0.0;
+            else if (idx == NSS + 1) v = l == 0 ? (double)pairs * 64.0 : 0.0;
+            ch[k * kStatStride + l] = v;
         }
         wave_sync();
-        const int k = l >> 3, part = l & 7;
+        const int k = l >> 4, part = l & 15;
         double sum = 0.0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) sum += ch[k * CHS + u * 8 + part];
+        for (int u = 0; u < 4; ++u) sum += ch[k * kStatStride + u * 16 + part];
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
         sum += __shfl_xor(sum, 4);
+        sum += __shfl_xor(sum, 8);
         if (part == 0 && c0 + k < NSX) s_wstat[w][c0 + k] = sum;
         wave_sync();
     }
+    S.mark(6);
+#ifdef GICP_STAMPS
+    if (A.stamps && l == 0)
+        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kWavesPerWG + w) * 8 + c] = S.acc[c];
+#endif
     __syncthreads();
     if (threadIdx.x < NSX) {
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < kWavesPerWG; ++u) s += s_wstat[u][threadIdx.x];
-        A.partials[(int64_t)blockIdx.x * NSX + threadIdx.x] = s;
+        A.partials[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;   // [statistic][workgroup]
     }
 }
 
-// Deterministic sum of the per-workgroup partials: one workgroup per statistic.
+// Deterministic sum of the per-workgroup partials ([statistic][workgroup]): one workgroup per statistic.
 __global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ partials, int nparts, int nsx,
                                                  double* __restrict__ out) {
     __shared__ double sh[256];
     const int v = blockIdx.x;
+    const double* row = partials + (int64_t)v * nparts;
     double s = 0.0;
-    for (int p = threadIdx.x; p < nparts; p += 256) s += partials[(int64_t)p * nsx + v];
+    for (int p = threadIdx.x; p < nparts; p += 256) s += row[p];
     sh[threadIdx.x] = s;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {

@@ -234,6 +234,33 @@ def _cg_inner(stats, offset, T_k):
     return out[0], out[1]
 
 
+def _loss_2d(x, s, q, W):
+    """The reference's loss (gicp.py:52-58) on GPU-produced correspondences q and weights W."""
+    r = q - s @ _rot2(x[2]).T - x[:2]
+    wr = np.sum(W * r[:, None, :], axis=2)
+    return np.sum(r * wr)
+
+
+def _grad_2d(x, s, q, W):
+    """The reference's gradient (gicp.py:60-76)."""
+    r = q - s @ _rot2(x[2]).T - x[:2]
+    wr = np.sum(W * r[:, None, :], axis=2)
+    g = np.zeros(3)
+    g[:2] = -2 * np.sum(wr, axis=0)
+    dR = np.array([[-np.sin(x[2]), -np.cos(x[2])], [np.cos(x[2]), -np.sin(x[2])]])
+    g[2] = np.sum(-2 * (wr.T @ s) * dR)
+    return g
+
+
+def _cg_inner_faithful(src, q, W, offset):
+    """fmin_cg on the per-point loss exactly as gicp.py:148-154 evaluates it."""
+    from scipy.optimize import fmin_cg
+
+    out = fmin_cg(f=lambda x: _loss_2d(x, src, q, W), x0=offset, fprime=lambda x: _grad_2d(x, src, q, W),
+                  disp=False, full_output=True)
+    return out[0], out[1]
+
+
 _ENGINES = {}
 
 
@@ -245,24 +272,36 @@ def _engine(device):
 
 
 def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
-         max_distance_nearest_neighbors=50, *, full_output=True, inner=None, k_neighbors=None, device=0,
+         max_distance_nearest_neighbors=50, *, full_output=True, mode=None, inner=None, k_neighbors=None, device=0,
          verbose=True, T0=None):
     """Drop-in for gicp.py:78 — returns the same 7-tuple (gicp.py:174):
 
     (T, all_transformations, initial_source_cov_matrices, target_cov_matrices,
      highest_weight_points_source, highest_weight_points_target, all_source_cov_matrices)
 
-    2-D and 3-D clouds (T is 3x3 or 4x4).  ``inner``: 'cg' (2-D default:
-    scipy fmin_cg on the GPU-reduced closed form, reproducing the reference's
-    inexact inner stop) or 'newton' (exact minimiser on SO(d); 3-D default).
-    ``full_output=False`` skips the per-point visualisation extras (the lists
-    come back empty), which is what large clouds want.
+    2-D and 3-D clouds (T is 3x3 or 4x4).
+
+    mode='faithful' (2-D default): every iteration the GPU recomputes the source
+      covariances on the transformed source (gicp.py:120) and produces the
+      correspondences and weights; scipy's fmin_cg then minimises the
+      reference's own per-point loss on them (gicp.py:148-154), so the inexact
+      inner stop follows the reference's trajectory.
+    mode='fast' (3-D default, and any large cloud): source covariances are
+      rotated (rigid invariance), the GPU reduces the loss to its sufficient
+      statistics in one pass, and the inner problem is solved on the host from
+      them -- by fmin_cg on the closed form (inner='cg', 2-D) or exactly by
+      Newton on SO(d) (inner='newton').
+    full_output=False skips the per-point visualisation extras (the three
+    lists come back empty), which is what large clouds want.
     """
     src = Engine._cloud(source_points)
     tgt = Engine._cloud(target_points)
     d = src.shape[1]
     if tgt.shape[1] != d:
         raise ValueError("source and target must have the same dimension")
+    mode = ("faithful" if d == 2 else "fast") if mode is None else mode
+    if mode not in ("faithful", "fast") or (mode == "faithful" and d != 2):
+        raise ValueError("mode must be 'fast', or 'faithful' for 2-D clouds")
     inner = ("cg" if d == 2 else "newton") if inner is None else inner
     if inner not in ("cg", "newton") or (inner == "cg" and d != 2):
         raise ValueError("inner must be 'newton', or 'cg' for 2-D clouds")
@@ -271,34 +310,52 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
                        max_distance_correspondence=float(max_distance_correspondence),
                        max_distance_nearest_neighbors=float(max_distance_nearest_neighbors), k_neighbors=k_neighbors)
     eng.set_target(tgt, p)
-    eng.set_source(src, p)
     target_cov = eng.covariances("target")
+    eng.set_source(src, p)
     init_src_cov = eng.covariances("source")
     T = np.eye(d + 1) if T0 is None else np.array(T0, dtype=np.float64)
     all_T = [T]
     offset = np.array([T[0, 2], T[1, 2], np.arctan2(T[1, 0], T[0, 0])]) if d == 2 else None
     last = np.inf
     hw_s, hw_t, all_src_cov = [], [], []
+    eye = np.eye(d + 1)
     for it in range(int(max_iterations)):
-        if full_output:
-            st, dbg = eng.iterate(T, debug=True)
-            R = T[:d, :d]
-            all_src_cov.append(np.einsum("ab,nbc,dc->nad", R, init_src_cov, R))
+        moved = apply_transformation(src, T)                       # gicp.py:119
+        if mode == "faithful":
+            if it > 0:
+                eng.set_source(moved, p)                           # gicp.py:120, on the GPU
+            cs = eng.covariances("source") if it > 0 else init_src_cov
+            if full_output:
+                all_src_cov.append(cs)
+            _, dbg = eng.iterate(eye, debug=True)                  # gicp.py:124-145 on the moved cloud
+            idx = dbg["index"]
+            q = np.zeros_like(src)
+            q[idx >= 0] = tgt[idx[idx >= 0]]
+            if inner == "cg":
+                new_offset, min_loss = _cg_inner_faithful(src, q, dbg["weight"], offset)
+                T_new = _offset_to_T(new_offset)
+            else:
+                T_new, min_loss = _newton_from_points(src, q, dbg["weight"], idx, T)
+                new_offset = None
         else:
-            st = eng.iterate(T)
-        if inner == "cg":
-            new_offset, min_loss = _cg_inner(st, offset, T)
-            T_new = _offset_to_T(new_offset)
-        else:
-            T_new, min_loss = solve_pose(st, T)
-            new_offset = None
+            if full_output:
+                st, dbg = eng.iterate(T, debug=True)
+                R = T[:d, :d]
+                all_src_cov.append(np.einsum("ab,nbc,dc->nad", R, init_src_cov, R))
+            else:
+                st = eng.iterate(T)
+            if inner == "cg":
+                new_offset, min_loss = _cg_inner(st, offset, T)
+                T_new = _offset_to_T(new_offset)
+            else:
+                T_new, min_loss = solve_pose(st, T)
+                new_offset = None
         if abs(last - min_loss) < tolerance:                       # gicp.py:155-162
             if verbose:
                 print("Converged at iteration", it)
             break
         last = min_loss
         if full_output:                                            # gicp.py:169-172
-            moved = apply_transformation(src, T)
             idx = dbg["index"]
             q = np.zeros_like(src)
             q[idx >= 0] = tgt[idx[idx >= 0]]
@@ -308,4 +365,21 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
         offset = new_offset
         T = T_new
         all_T.append(T)
+    if mode == "faithful":
+        eng.set_source(src, p)   # leave the engine holding the untransformed source
     return T, all_T, init_src_cov, target_cov, hw_s, hw_t, all_src_cov
+
+
+def _newton_from_points(src, q, W, idx, T):
+    """Exact inner minimiser for the faithful path: statistics of the given (q, W) at T, then the host solve."""
+    d = src.shape[1]
+    ok = idx >= 0
+    s, qq, WW = src[ok], q[ok], W[ok]
+    r = qq - s @ T[:d, :d].T - T[:d, d]
+    wr = np.einsum("nab,nb->na", WW, r)
+    P = _sym_pairs(d)
+    ws = np.stack([WW[:, a, b] for a, b in P], axis=1)
+    ss = np.stack([s[:, i] * s[:, j] for i, j in P], axis=1)
+    st = np.concatenate([np.einsum("np,nq->pq", ws, ss).ravel(), np.einsum("np,ni->pi", ws, s).ravel(), ws.sum(0),
+                         np.einsum("na,ni->ai", wr, s).ravel(), wr.sum(0), [np.sum(r * wr)], [float(ok.sum())]])
+    return solve_pose(st, T)

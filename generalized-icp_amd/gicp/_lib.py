@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgicp_hip.so")
+# GICP_LIB_VARIANT=stamps loads the diagnostic build with in-kernel phase timers (make STAMPS=1)
+LIB_PATH = os.path.join(HERE, "libgicp_hip_stamps.so" if os.environ.get("GICP_LIB_VARIANT") == "stamps"
+                        else "libgicp_hip.so")
 
 GICP_OK = 0
 GICP_E_INVALID = -1

@@ -56,6 +56,19 @@ def test_iteration_2d_vs_reference(eng, name):
         assert np.max(np.abs(st - ref) / scale) < 1e-7, k
 
 
+STABLE = ["vis_s3", "robot_p0_r90", "robot_p2_r90", "robot_p0_r360", "robot_p2_r360", "segment_2k"]
+
+
+@pytest.mark.parametrize("name", STABLE)
+def test_gicp_2d_fast_mode_in_reference_ensemble(name):
+    """The closed-form path (one GPU reduction per iteration + fmin_cg on the statistics) on the
+    fixtures where the reference endpoint is stable under input perturbation."""
+    fx = load(name)
+    T, *_ = gicp.gicp(fx["source"], fx["target"], mode="fast", full_output=False, verbose=False, **kwargs(fx))
+    ok, best = in_ensemble(T, fx["ens_T"])
+    assert ok, best
+
+
 @pytest.mark.parametrize("name", [n for n in NAMES if n not in DIVERGENT])
 def test_gicp_2d_end_to_end_in_reference_ensemble(name, capsys):
     """Drop-in gicp() on the GPU lands within 1e-4 rad / 1e-3 px of the reference's endpoint ensemble."""
@@ -69,6 +82,10 @@ def test_gicp_2d_end_to_end_in_reference_ensemble(name, capsys):
     n_exec = len(all_cov)
     assert len(all_T) == (n_exec + 1 if n_exec == int(fx["max_iterations"]) and len(all_T) > n_exec else n_exec)
     assert len(hw_s) == len(all_T) - 1 and hw_s[0].shape == (5, 2)
+    np.testing.assert_allclose(tgt_cov, fx["tgt_cov"], atol=1e-10)
+    np.testing.assert_allclose(init_cov, fx["init_src_cov"], atol=1e-10)
+    k = min(len(all_cov), len(fx["all_src_cov"]))
+    np.testing.assert_allclose(all_cov[0], fx["all_src_cov"][0], atol=1e-10)
     if np.allclose(T, fx["T"], atol=1e-6):
         # |delta loss| < 1e-6 on losses ~1e3 decides at the 1e-9 relative level, below the rounding
         # difference of any two evaluations of the loss: the stop may come one iteration apart
