@@ -85,6 +85,7 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())   # rehearsal on fewer GPUs than ranks
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import gicp
