@@ -17,12 +17,16 @@ constexpr int kTile = 64;          // points per tile (= one wave of queries)
 constexpr int kBlockTiles = 64;    // tiles per block (= one wave of tile tests)
 constexpr int kWavesPerWG = 4;     // 256-thread workgroups, each wave independent
 
+constexpr int kSub = 4;            // 16-row sub-tiles per tile (finer culling of the row scan)
+
 struct __attribute__((aligned(16))) TileInfo {
     double c[3];      // fp64 centre (midpoint of the fp64 AABB)
     float h[3];       // half-extents: max |rel32| over the tile's points, per axis
     int32_t start;    // first sorted point
     int32_t count;    // 1..64
     float radius;     // max |rel32| norm
+    float sc[kSub][3];  // sub-tile box centres (rows 16g..16g+15), relative to c, fp32
+    float sh[kSub][3];  // sub-tile box half-extents (cover every rel32 of the sub-tile)
 };
 
 struct __attribute__((aligned(16))) BlockInfo {

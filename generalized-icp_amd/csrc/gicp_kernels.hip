@@ -33,7 +33,10 @@ __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
     return max(min(a, b), min(max(a, b), c));
 }
 __device__ __forceinline__ float key_d2(unsigned k) { return __uint_as_float(k & ~63u); }
-__device__ __forceinline__ float marg(const Margin& m, float d2) { return fmaf(m.a, sqrtf(d2), fmaf(m.c, d2, m.b)); }
+// margin of the fp32 screen at d2 (raw v_sqrt_f32, inflated past its 1-ulp error: the bound stays conservative)
+__device__ __forceinline__ float marg(const Margin& m, float d2) {
+    return fmaf(m.a * 1.0001f, __builtin_amdgcn_sqrtf(d2), fmaf(m.c, d2, m.b));
+}
 
 // wave-wide max, result uniform (SGPR): DPP row_shr 1/2/4/8, row_bcast 15/31, readlane 63
 __device__ __forceinline__ float wave_maxf(float v) {
@@ -167,6 +170,28 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
     float h[3];
     for (int a = 0; a < 3; ++a) h[a] = wave_maxf(fabsf(r[a]));
     const float rad = wave_maxf(sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]));
+    // 16-row sub-tile boxes (min/max over each 16-lane row of the wave)
+    float smn[3], smx[3];
+    for (int a = 0; a < 3; ++a) {
+        smn[a] = v ? r[a] : 3e38f;
+        smx[a] = v ? r[a] : -3e38f;
+        for (int o = 1; o < 16; o <<= 1) {
+            smn[a] = fminf(smn[a], __shfl_xor(smn[a], o));
+            smx[a] = fmaxf(smx[a], __shfl_xor(smx[a], o));
+        }
+    }
+    if ((l & 15) == 0) {
+        const int g = l >> 4;
+        TileInfo& t = tiles[T];
+        for (int a = 0; a < 3; ++a) {
+            const bool empty = smn[a] > smx[a];
+            const float cc = empty ? 0.f : 0.5f * (smn[a] + smx[a]);
+            // half-extent rounded up so the box covers both extremes exactly
+            const float hh = empty ? -1e30f : fmaxf(smx[a] - cc, cc - smn[a]) * (1.0f + 2.4e-7f);
+            t.sc[g][a] = cc;
+            t.sh[g][a] = hh;
+        }
+    }
     if (l == 0) {
         TileInfo& t = tiles[T];
         for (int a = 0; a < 3; ++a) {
@@ -268,15 +293,18 @@ __device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, 
 }
 
 // per-wave LDS: tile staging during the walk, statistics transpose afterwards (same bytes)
-constexpr int kStatCh = 4;        // statistics per reduction round
-constexpr int kStatStride = 80;   // doubles per statistic row: conflict-free for the 16-lane reads
 struct WaveStage {
     float x[kTile], y[kTile], z[kTile];           // fp32 screen coordinates, SoA
     double x64[kTile], y64[kTile], z64[kTile];    // fp64 coordinates (covariance sums, fallback)
 };
+// statistics transpose image: 16 points x 16 u-terms and 16 x 16 v-terms (XOR-swizzled 16-B chunks)
+struct WaveStat {
+    double u[16 * 16];
+    double v[16 * 16];
+};
 union __attribute__((aligned(16))) WaveLds {
     WaveStage t;
-    double chunk[kStatCh * kStatStride];
+    WaveStat st;
 };
 
 // Lane point relative to database tile T, and the per-lane squared gap to T's box.
@@ -294,9 +322,28 @@ __device__ __forceinline__ float lane_gap2(const Query<D>& q, const TileInfo& ti
     return g2;
 }
 
-// uniform (scalar-cache) copy of a tile's metadata
+// uniform copy of a tile's metadata through the constant address space: scalar s_load_dwordx*
+// into SGPRs (a generic pointer here compiles to ten vector loads + readfirstlane)
+typedef __attribute__((address_space(4))) const TileInfo* ConstTiles;
 __device__ __forceinline__ TileInfo tile_meta(const DevCloud& db, int T) {
-    return db.tiles[__builtin_amdgcn_readfirstlane(T)];
+    const ConstTiles ct = (ConstTiles)(uintptr_t)db.tiles + __builtin_amdgcn_readfirstlane(T);
+    TileInfo t;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        t.c[a] = ct->c[a];
+        t.h[a] = ct->h[a];
+    }
+    t.start = ct->start;
+    t.count = ct->count;
+    t.radius = ct->radius;
+#pragma unroll
+    for (int g = 0; g < kSub; ++g)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            t.sc[g][a] = ct->sc[g][a];
+            t.sh[g][a] = ct->sh[g][a];
+        }
+    return t;
 }
 
 // stage a tile's fp32 coordinates (padding rows at 1e30: their distance is +inf)
@@ -360,17 +407,48 @@ __device__ __forceinline__ void scan_group(const WaveLds& L, const float* pr, un
 }
 
 template <int D, class Row, int... G>
-__device__ __forceinline__ void scan_groups(const WaveLds& L, int n4, const float* pr, unsigned M, Row& row,
-                                            std::integer_sequence<int, G...>) {
-    // short-circuit fold: group G runs only while 4G < n4 (wave-uniform branch)
-    (void)((4 * G < n4 ? (scan_group<4 * G, D>(L, pr, M, row), true) : false) && ...);
+__device__ __forceinline__ void scan_groups(const WaveLds& L, int n4, unsigned sub, const float* pr, unsigned M,
+                                            Row& row, std::integer_sequence<int, G...>) {
+    // short-circuit fold: group G runs only while 4G < n4; skipped when its 16-row sub-tile is not needed
+    (void)((4 * G < n4 ? (((sub >> (G / 4)) & 1u) ? scan_group<4 * G, D>(L, pr, M, row) : void(), true) : false) &&
+           ...);
 }
 
-// Scan one staged tile: row(key, j) for every row; key = (d2 bits & ~63) | row.
+// Per-lane squared gap to each 16-row sub-box of the staged tile; bit g of the result is set when
+// some lane within its bound needs sub-tile g.  Same conservative slack as lane_gap2.
+template <int D>
+__device__ __forceinline__ unsigned sub_mask(const TileInfo& ti, const float* pr, bool valid, float bound) {
+    unsigned m = 0;
+#pragma unroll
+    for (int g = 0; g < kSub; ++g) {
+        if (16 * g >= ti.count) break;
+        float g2 = 0.f;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const float dl = fabsf(pr[a] - ti.sc[g][a]);
+            float gg = dl - ti.sh[g][a] - (dl + ti.sh[g][a] + fabsf(pr[a])) * 9.5367431640625e-7f;
+            gg = fmaxf(gg, 0.f);
+            g2 = fmaf(gg, gg, g2);
+        }
+        if (__any(valid && g2 <= bound)) m |= 1u << g;
+    }
+    return m;
+}
+
+__device__ __forceinline__ int rows_scanned(unsigned sub, int count) {
+    int r = 0;
+#pragma unroll
+    for (int g = 0; g < kSub; ++g)
+        if ((sub >> g) & 1u) r += min(16, max(0, ((count + 3) & ~3) - 16 * g));
+    return r;
+}
+
+// Scan one staged tile: row(key, j) for every row of the sub-tiles in `sub`; key = (d2 bits & ~63) | row.
 template <int D, class Row>
-__device__ __forceinline__ void scan_tile(const WaveLds& L, int count, const float* pr, Row&& row) {
+__device__ __forceinline__ void scan_tile(const WaveLds& L, int count, const float* pr, Row&& row,
+                                          unsigned sub = 0xFu) {
     const unsigned M = key_mask();
-    scan_groups<D>(L, (count + 3) & ~3, pr, M, row, std::make_integer_sequence<int, kTile / 4>{});
+    scan_groups<D>(L, (count + 3) & ~3, sub, pr, M, row, std::make_integer_sequence<int, kTile / 4>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -477,7 +555,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
     if (T >= A.q_end) return;  // waves are independent (no workgroup barrier here)
     WaveLds& L = s_lds[w];
     const DevCloud& cl = A.cl;
-    const TileInfo qt = cl.tiles[T];
+    const TileInfo qt = tile_meta(cl, T);
 
     Query<D> q;
     q.valid = l < qt.count;
@@ -704,30 +782,25 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
     int pairs = 0;
 
     if (active) {
-        const TileInfo st = sc.tiles[T];
+        const TileInfo st = tile_meta(sc, T);
         Query<D> q;
         q.valid = l < st.count;
         const int i = st.start + min(l, st.count - 1);
         const float4 rel = sc.rel32[i];
-        const double4 s4 = reinterpret_cast<const double4*>(sc.xyz64)[i];
         const float relv[3] = {rel.x, rel.y, rel.z};
-        const double s4v[3] = {s4.x, s4.y, s4.z};
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            double o = A.t[a], p = A.t[a];
+            double o = A.t[a];
             float pw = 0.f, ew = 0.f;
 #pragma unroll
             for (int b = 0; b < D; ++b) {
                 o += A.R[a * D + b] * st.c[b];
-                p += A.R[a * D + b] * s4v[b];
                 pw = fmaf(A.R32[a * D + b], relv[b], pw);
                 ew = fmaf(fabsf(A.R32[a * D + b]), st.h[b], ew);
             }
             q.ow[a] = o;
-            q.p64[a] = p;
             q.pw[a] = pw;
             q.ew[a] = ew * (1.0f + 4.8e-7f) + 1e-30f;
-            sv[a] = s4v[a];
         }
 
         // seed: last pass's best target tile for this source tile, else the Morton neighbour
@@ -752,22 +825,25 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             const float b = key_d2(best);
             return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
         };
+        float lb = lane_bound();   // refreshed after every merge
         auto visit = [&](int Tt) -> bool {
             S.mark(1);
             const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
-            const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
+            const bool need = lane_gap2<D>(q, ti, pr) <= lb;
             if (!__any(need)) {
                 S.mark(2);
                 return false;
             }
+            const unsigned sub = sub_mask<D>(ti, pr, q.valid, lb);
             stage_f32(tg, ti, L);
             S.mark(2);
             unsigned tb = 0xFFFFFFFFu, ts = 0xFFFFFFFFu;
             scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
                 ts = umed3(tb, ts, key);
                 tb = min(tb, key);
-            });
+            }, sub);
+            pairs += rows_scanned(sub, ti.count);
             if (tb < best) {
                 sec = min(best, ts);
                 best = tb;
@@ -775,15 +851,28 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             } else {
                 sec = min(sec, tb);
             }
-            pairs += ti.count;
+            lb = lane_bound();
             wave_sync();
             S.mark(3);
             return true;
         };
         S.mark(0);
-        traverse<D>(tg, q, seed, visit, [&]() { return wave_maxf(lane_bound()); });
+        traverse<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); });
         S.mark(1);
 
+        // the fp64 source point is needed only from here on (kept out of the walk's registers)
+        {
+            const double4 s4 = reinterpret_cast<const double4*>(sc.xyz64)[i];
+            const double s4v[3] = {s4.x, s4.y, s4.z};
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                double p = A.t[a];
+#pragma unroll
+                for (int b = 0; b < D; ++b) p += A.R[a * D + b] * s4v[b];
+                q.p64[a] = p;
+                sv[a] = s4v[a];
+            }
+        }
         const bool found = q.valid && best < init;
         int j = -1;
         double d2e = 0.0;
@@ -856,7 +945,7 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
 #pragma unroll
                     for (int b = 0; b < D; ++b)
                         S[a][b] = (a == b ? cs.x + ct.x : 0.0) - mr[a] * mr[b] - mt[a] * mt[b];
-                if (D == 2) {
+                if constexpr (D == 2) {
                     const double det = S[0][0] * S[1][1] - S[0][1] * S[1][0];
                     W[0][0] = S[1][1] / det;
                     W[1][1] = S[0][0] / det;
@@ -905,31 +994,76 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
     }
 
     S.mark(5);
-    // ---- wave reduction of the statistics: 4 at a time through LDS (reusing the stage bytes)
-    wave_sync();
-    double* ch = s_lds[w].chunk;
+    // ---- wave reduction of the statistics: a 16x16x64 fp64 GEMM on MFMA ---------------------
+    // stats[p][q] = sum over lanes of u_p v_q with u = (W sym, W r, r^T W r, 1), v = (s s sym, s, 1)
+    // (DESIGN.md §4).  Points are transposed through LDS 16 at a time (rows of 16 doubles, 16-B
+    // chunks XOR-swizzled by row so the 8-lane write groups and 32-lane read groups are conflict-free);
+    // lane l feeds A[p = l&15][k = l>>4] / B[k][q = l&15] of v_mfma_f64_16x16x4_f64.
+    {
+        constexpr int NS = D * (D + 1) / 2;
+        // u_k / v_k of this lane's point, formed at the write (k is a compile-time constant there)
+        auto uel = [&](int k) -> double {
+            if (!on) return 0.0;
+            if (k < NS) return W[StatIdx<D>::pa(k)][StatIdx<D>::pb(k)];
+            if (k < NS + D) return wr[k - NS];
+            if (k == NS + D) return rwr;
+            if (k == NS + D + 1) return 1.0;
+            return 0.0;
+        };
+        auto vel = [&](int k) -> double {
+            if (!on) return 0.0;
+            if (k < NS) return sv[StatIdx<D>::pa(k)] * sv[StatIdx<D>::pb(k)];
+            if (k < NS + D) return sv[k - NS];
+            if (k == NS + D) return 1.0;
+            return 0.0;
+        };
+        typedef double d4v __attribute__((ext_vector_type(4)));
+        d4v acc = {0.0, 0.0, 0.0, 0.0};
+        WaveStat& X = s_lds[w].st;
+        const int row = l & 15;
+        wave_sync();
 #pragma unroll
-    for (int c0 = 0; c0 < NSX; c0 += kStatCh) {
+        for (int g = 0; g < 4; ++g) {
+            if ((l >> 4) == g) {
 #pragma unroll
-        for (int k = 0; k < kStatCh; ++k) {
-            const int idx = c0 + k;
-            double v = 0.0;
-            if (idx < NSS) v = on ? stat_value<D>(idx, W, sv, wr, rwr) : 0.0;
-            else if (idx == NSS) v = amb ? 1.0 : 0.0;
-            else if (idx == NSS + 1) v = l == 0 ? (double)pairs * 64.0 : 0.0;
-            ch[k * kStatStride + l] = v;
+                for (int c = 0; c < 8; ++c) {
+                    const int off = row * 16 + 2 * (c ^ (row & 7));
+                    *reinterpret_cast<double2*>(&X.u[off]) = make_double2(uel(2 * c), uel(2 * c + 1));
+                    *reinterpret_cast<double2*>(&X.v[off]) = make_double2(vel(2 * c), vel(2 * c + 1));
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int r = 4 * cc + (l >> 4);
+                const int e = l & 15;
+                const int off = r * 16 + 2 * ((e >> 1) ^ (r & 7)) + (e & 1);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X.u[off], X.v[off], acc, 0, 0, 0);
+            }
+            wave_sync();
         }
-        wave_sync();
-        const int k = l >> 4, part = l & 15;
-        double sum = 0.0;
+        // lane l holds stats[p = (l>>4) + 4j][q = l&15], j = 0..3
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sum += ch[k * kStatStride + u * 16 + part];
-        sum += __shfl_xor(sum, 1);
-        sum += __shfl_xor(sum, 2);
-        sum += __shfl_xor(sum, 4);
-        sum += __shfl_xor(sum, 8);
-        if (part == 0 && c0 + k < NSX) s_wstat[w][c0 + k] = sum;
-        wave_sync();
+        for (int j = 0; j < 4; ++j) {
+            const int p = (l >> 4) + 4 * j, qq = l & 15;
+            int idx = -1;
+            if (p < NS) {
+                if (qq < NS) idx = p * NS + qq;
+                else if (qq < NS + D) idx = NS * NS + p * D + (qq - NS);
+                else if (qq == NS + D) idx = NS * NS + NS * D + p;
+            } else if (p < NS + D) {
+                if (qq >= NS && qq < NS + D) idx = NS * NS + NS * D + NS + (p - NS) * D + (qq - NS);
+                else if (qq == NS + D) idx = NS * NS + NS * D + NS + D * D + (p - NS);
+            } else if (qq == NS + D && p <= NS + D + 1) {
+                idx = NS * NS + NS * D + NS + D * D + D + (p - NS - D);   // c0, count
+            }
+            if (idx >= 0) s_wstat[w][idx] = acc[j];
+        }
+        const int namb = (int)__popcll(__ballot(amb));
+        if (l == 0) {
+            s_wstat[w][NSS] = (double)namb;
+            s_wstat[w][NSS + 1] = (double)pairs * 64.0;
+        }
     }
     S.mark(6);
 #ifdef GICP_STAMPS
