@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <new>
@@ -27,9 +28,9 @@ hipError_t launch_build_tiles(const double*, int, const int32_t*, TileInfo*, int
                               unsigned*, hipStream_t);
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
-hipError_t launch_corr(const CorrArgs&, int, hipStream_t);
+hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_reduce(const double*, int, int, double*, hipStream_t);
-int corr_grid(int);
+int corr_grid(int, int);
 int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
 }  // namespace gicp
 
@@ -135,6 +136,15 @@ struct gicp_ctx {
     double* d_dbg_w = nullptr;
     double* d_dbg_dist = nullptr;
     size_t dbg_cap = 0;
+    // per-source-tile candidate lists
+    int32_t* d_list = nullptr;
+    int32_t* d_list_len = nullptr;
+    int32_t* d_list_pass = nullptr;
+    float* d_list_rcert = nullptr;
+    double* d_poses = nullptr;
+    int pass = 0;
+    bool use_lists = true;
+    double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -353,13 +363,22 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     c->nshards = nshards;
     c->q_begin = (int)((int64_t)c->src.ntiles * shard / nshards);
     c->q_end = (int)((int64_t)c->src.ntiles * (shard + 1) / nshards);
-    dalloc(c->d_hint, std::max(1, c->src.ntiles));
-    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * std::max(1, c->src.ntiles), c->stream));
+    const int nt = std::max(1, c->src.ntiles);
+    dalloc(c->d_hint, nt);
+    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * nt, c->stream));
+    dalloc(c->d_list, (size_t)nt * kListMax);
+    dalloc(c->d_list_len, nt);
+    dalloc(c->d_list_pass, nt);
+    dalloc(c->d_list_rcert, nt);
+    if (!c->d_poses) dalloc(c->d_poses, (size_t)kPoseRing * 12);
+    HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
+    c->pass = 0;
 }
 
 void ensure_workspace(gicp_ctx* c) {
     const int nsx = nstat_ext(3);
-    const size_t need = (size_t)std::max(1, corr_grid(c->q_end - c->q_begin)) * nsx;
+    const size_t need = (size_t)std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim)) * nsx;
     if (need > c->partials_cap) {
         dalloc(c->d_partials, need);
         c->partials_cap = need;
@@ -395,6 +414,14 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     a.hint = c->d_hint;
     a.partials = c->d_partials;
     a.count_pairs = 1;
+    a.list = c->d_list;
+    a.list_len = c->d_list_len;
+    a.list_rcert = c->d_list_rcert;
+    a.list_pass = c->d_list_pass;
+    a.poses = c->d_poses;
+    a.pass = ++c->pass;
+    a.use_lists = c->use_lists ? 1 : 0;
+    a.skin = (float)(0.2 * dc);
     if (dbg && (dbg->index || dbg->weight || dbg->distance)) {
         const size_t n = (size_t)c->src.n;
         if (c->dbg_cap < n) {
@@ -408,12 +435,12 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
         a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
     }
     const int nsx = nstat_ext(d);
-    const int grid = corr_grid(c->q_end - c->q_begin);
+    const int grid = corr_grid(c->q_end - c->q_begin, d);
     hipStream_t st = c->stream;
 #ifdef GICP_STAMPS
     static unsigned long long* d_stamps = nullptr;
     static size_t stamps_cap = 0;
-    const size_t nst = (size_t)std::max(1, grid) * kWavesPerWG * 8;
+    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 8;
     if (nst > stamps_cap) {
         dalloc(d_stamps, nst);
         stamps_cap = nst;
@@ -422,7 +449,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     a.stamps = d_stamps;
 #endif
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], st));
-    if (grid > 0) HIPCHK(launch_corr(a, d, st));
+    if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
     if (c->timing) HIPCHK(hipEventRecord(c->ev[1], st));
     if (grid > 0) HIPCHK(launch_reduce(c->d_partials, grid, nsx, c->d_stats, st));
     else HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(double) * nsx, st));
@@ -453,14 +480,44 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
         int nw = 0;
         for (size_t w = 0; w < nst / 8; ++w) {
             unsigned long long r = 0;
-            for (int k = 0; k < 8; ++k) r += hs[w * 8 + k];
+            for (int k = 0; k < 7; ++k) r += hs[w * 8 + k];
             if (!r) continue;
             ++nw;
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < 7; ++k) {
                 tot[k] += (double)hs[w * 8 + k];
                 all += (double)hs[w * 8 + k];
             }
         }
+        {   // slowest 1% of waves vs the rest: phase mix and rows scanned
+            std::vector<std::pair<double, size_t>> byc;
+            for (size_t w = 0; w < nst / 8; ++w) {
+                double r = 0;
+                for (int k = 0; k < 7; ++k) r += (double)hs[w * 8 + k];
+                if (r > 0) byc.push_back({r, w});
+            }
+            std::sort(byc.begin(), byc.end());
+            const size_t n1 = std::max<size_t>(1, byc.size() / 100);
+            double slow[8] = {0}, med[8] = {0};
+            for (size_t i = 0; i < n1; ++i)
+                for (int k = 0; k < 8; ++k) slow[k] += (double)hs[byc[byc.size() - 1 - i].second * 8 + k] / n1;
+            for (size_t i = byc.size() / 2 - n1 / 2, e = i + n1; i < e && i < byc.size(); ++i)
+                for (int k = 0; k < 8; ++k) med[k] += (double)hs[byc[i].second * 8 + k] / n1;
+            std::fprintf(stderr, "[stamps] slowest1%%: rows %.0f setup %.0f trav %.0f stage %.0f scan %.0f fb %.0f epi %.0f red %.0f | median: rows %.0f setup %.0f trav %.0f stage %.0f scan %.0f fb %.0f epi %.0f red %.0f\n",
+                         slow[7], slow[0], slow[1], slow[2], slow[3], slow[4], slow[5], slow[6], med[7], med[0], med[1],
+                         med[2], med[3], med[4], med[5], med[6]);
+        }
+        std::vector<double> per;
+        per.reserve(nst / 8);
+        for (size_t w = 0; w < nst / 8; ++w) {
+            unsigned long long r = 0;
+            for (int k = 0; k < 7; ++k) r += hs[w * 8 + k];
+            if (r) per.push_back((double)r);
+        }
+        std::sort(per.begin(), per.end());
+        if (!per.empty())
+            std::fprintf(stderr, "[stamps] wave cycles p50 %.0f p90 %.0f p99 %.0f p999 %.0f max %.0f\n",
+                         per[per.size() / 2], per[per.size() * 9 / 10], per[per.size() * 99 / 100],
+                         per[per.size() * 999 / 1000], per.back());
         static const char* nm[8] = {"setup", "traverse", "need+stage", "scan", "fallback", "epilogue", "reduce", "-"};
         std::fprintf(stderr, "[stamps] waves %d, mean cycles/wave %.0f:", nw, all / std::max(1, nw));
         for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * tot[k] / std::max(1.0, all));
@@ -470,6 +527,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     const int ns = nstat(d);
     c->last_amb = c->h_stats[ns];
     c->last_pairs = c->h_stats[ns + 1];
+    c->last_rebuilds = c->h_stats[ns + 2];
 }
 
 }  // namespace
@@ -521,6 +579,7 @@ int gicp_create(gicp_ctx** out, int device) {
     gicp_ctx* c = new (std::nothrow) gicp_ctx();
     if (!c) return GICP_E_NOMEM;
     c->device = device;
+    if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;
@@ -558,6 +617,11 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_dbg_idx);
     dfree(c->d_dbg_w);
     dfree(c->d_dbg_dist);
+    dfree(c->d_list);
+    dfree(c->d_list_len);
+    dfree(c->d_list_pass);
+    dfree(c->d_list_rcert);
+    dfree(c->d_poses);
     if (c->h_stats) (void)hipHostFree(c->h_stats);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);

@@ -16,7 +16,17 @@ constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kTile = 64;          // points per tile (= one wave of queries)
 constexpr int kBlockTiles = 64;    // tiles per block (= one wave of tile tests)
 constexpr int kWavesPerWG = 4;     // 256-thread workgroups, each wave independent
+#ifndef GICP_CORR_WAVES
+#define GICP_CORR_WAVES 4
+#endif
+#ifndef GICP_CORR_LOOP
+#define GICP_CORR_LOOP 0
+#endif
+constexpr int kCorrWaves = GICP_CORR_WAVES;       // waves per k_corr workgroup
+constexpr bool kCorrLoop = GICP_CORR_LOOP != 0;   // grid-stride over source tiles
 
+constexpr int kListMax = 64;       // candidate target tiles kept per source tile
+constexpr int kPoseRing = 64;      // passes a list stays usable for
 constexpr int kSub = 4;            // 16-row sub-tiles per tile (finer culling of the row scan)
 
 struct __attribute__((aligned(16))) TileInfo {
@@ -88,6 +98,17 @@ struct CorrArgs {
     double* dbg_weight;       // [N][dim][dim] (nullable)
     double* dbg_dist;         // [N] (nullable)
     int32_t count_pairs;      // 1: accumulate evaluated pairs (diagnostic)
+    // per-source-tile candidate lists (certified): built by a full walk with the
+    // search radius inflated by `skin`, reused while the tile's displacement since the build pose
+    // plus the wave's final search radius stays within the certified radius
+    int32_t* list;            // [src.ntiles][kListMax] target tiles
+    int32_t* list_len;        // [src.ntiles]
+    float* list_rcert;        // [src.ntiles] certified radius (0: invalid)
+    int32_t* list_pass;       // [src.ntiles] pass the list was built in
+    double* poses;            // [kPoseRing][12] pose of each pass (R row-major, t)
+    int32_t pass;             // this pass's id (monotonic per source cloud)
+    int32_t use_lists;        // 0: always full walk (no lists)
+    float skin;
     unsigned long long* stamps;  // [waves][8] phase cycles (STAMPS diagnostic build only; else null)
 };
 
@@ -95,6 +116,6 @@ constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;
 }
 // partials carry two extra diagnostics: ambiguous count, pairs evaluated
-constexpr int nstat_ext(int D) { return nstat(D) + 2; }
+constexpr int nstat_ext(int D) { return nstat(D) + 3; }   // + ambiguous, pairs, list rebuilds
 
 }  // namespace gicp

@@ -19,6 +19,7 @@
 // KD-tree exactly.  No MFMA: there is no dense contraction in this path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "gicp_internal.h"
@@ -36,6 +37,18 @@ __device__ __forceinline__ float key_d2(unsigned k) { return __uint_as_float(k &
 // margin of the fp32 screen at d2 (raw v_sqrt_f32, inflated past its 1-ulp error: the bound stays conservative)
 __device__ __forceinline__ float marg(const Margin& m, float d2) {
     return fmaf(m.a * 1.0001f, __builtin_amdgcn_sqrtf(d2), fmaf(m.c, d2, m.b));
+}
+
+// wave-wide min, result uniform (SGPR); same DPP pattern as wave_maxf
+__device__ __forceinline__ float wave_minf(float v) {
+    int x = __float_as_int(v);
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false))));
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false))));
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false))));
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false))));
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false))));
+    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false))));
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
 
 // wave-wide max, result uniform (SGPR): DPP row_shr 1/2/4/8, row_bcast 15/31, readlane 63
@@ -262,34 +275,67 @@ __device__ __forceinline__ float gap2_box(const Query<D>& q, const double* c, co
 // Two-level culled walk over the database tiles.  `visit(T)` returns true when it
 // processed the tile (the wave's bound then shrinks); `wave_bound()` is the max over
 // lanes of the squared search radius still needed.
-template <int D, class Visit, class WB>
-__device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, int seed, Visit&& visit,
-                                         WB&& wave_bound) {
+// With skin > 0 every tile whose box lies within sqrt(wb) + skin of the wave box is also passed
+// to collect(T) (wb as it stands when the tile is tested; wb only shrinks, so at the end the
+// collected set holds every tile within sqrt(wb_final) + skin).
+template <int D, class Visit, class WB, class Collect>
+__device__ __forceinline__ void traverse_c(const DevCloud& db, const Query<D>& q, int seed, Visit&& visit,
+                                           WB&& wave_bound, float skin, Collect&& collect) {
     const int l = lane_id();
+    auto infl = [&](float w) -> float {
+        if (skin <= 0.f || w < 0.f) return w;
+        const float r = __builtin_amdgcn_sqrtf(w) * 1.0001f + skin;
+        return r * r;
+    };
     float wb = wave_bound();
+    float wbi = infl(wb);
     if (seed >= 0) {
-        if (visit(seed)) wb = wave_bound();
+        collect(seed);
+        if (visit(seed)) {
+            wb = wave_bound();
+            wbi = infl(wb);
+        }
     }
     for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
         const int b = b0 + l;
         bool cb = false;
-        if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wb;
+        if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wbi;
         uint64_t bm = __ballot(cb);
         while (bm) {
             const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
             bm &= bm - 1;
             const int first = db.blocks[bb].first, nt = db.blocks[bb].ntiles;
             const int t = first + l;
-            bool ct = false;
-            if (l < nt && t != seed) ct = gap2_box<D>(q, db.tiles[t].c, db.tiles[t].h) <= wb;
-            uint64_t tm = __ballot(ct);
+            bool ct = false, cv = false;
+            if (l < nt && t != seed) {
+                const float g2 = gap2_box<D>(q, db.tiles[t].c, db.tiles[t].h);
+                ct = g2 <= wbi;
+                cv = g2 <= wb;
+            }
+            if (skin > 0.f) {
+                uint64_t cm = __ballot(ct);
+                while (cm) {
+                    collect(first + __ffsll((unsigned long long)cm) - 1);
+                    cm &= cm - 1;
+                }
+            }
+            uint64_t tm = __ballot(cv);
             while (tm) {
                 const int T = first + __ffsll((unsigned long long)tm) - 1;
                 tm &= tm - 1;
-                if (visit(T)) wb = wave_bound();
+                if (visit(T)) {
+                    wb = wave_bound();
+                    wbi = infl(wb);
+                }
             }
         }
     }
+}
+
+template <int D, class Visit, class WB>
+__device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, int seed, Visit&& visit,
+                                         WB&& wave_bound) {
+    traverse_c<D>(db, q, seed, visit, wave_bound, 0.f, [](int) {});
 }
 
 // per-wave LDS: tile staging during the walk, statistics transpose afterwards (same bytes)
@@ -351,6 +397,19 @@ __device__ __forceinline__ void stage_f32(const DevCloud& db, const TileInfo& ti
     const int l = lane_id();
     float4 v = make_float4(1e30f, 1e30f, 1e30f, 0.f);
     if (l < ti.count) v = db.rel32[ti.start + l];
+    L.t.x[l] = v.x;
+    L.t.y[l] = v.y;
+    L.t.z[l] = v.z;
+    wave_sync();
+}
+__device__ __forceinline__ float4 load_rel(const DevCloud& db, int start, int count) {
+    const int l = lane_id();
+    float4 v = make_float4(1e30f, 1e30f, 1e30f, 0.f);
+    if (l < count) v = db.rel32[start + l];
+    return v;
+}
+__device__ __forceinline__ void stage_f32_from(const float4& v, WaveLds& L) {
+    const int l = lane_id();
     L.t.x[l] = v.x;
     L.t.y[l] = v.y;
     L.t.z[l] = v.z;
@@ -761,27 +820,42 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 }
 
 template <int D>
-__global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
+__global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
     constexpr int NSS = nstat(D);
-    __shared__ WaveLds s_lds[kWavesPerWG];
-    __shared__ double s_wstat[kWavesPerWG][NSX];
+    __shared__ WaveLds s_lds[kCorrWaves];
+    __shared__ double s_wstat[kCorrWaves][NSX];   // per-wave statistics, accumulated over its tiles
 
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int T = A.q_begin + blockIdx.x * kWavesPerWG + w;
-    const bool active = T < A.q_end;
     WaveLds& L = s_lds[w];
     const DevCloud& sc = A.src;
     const DevCloud& tg = A.tgt;
 
     Stamps S;
     S.start();
+    if (A.use_lists && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
+        double* P = A.poses + (A.pass % kPoseRing) * 12;
+        for (int a = 0; a < 3; ++a) {
+            for (int b = 0; b < 3; ++b) P[a * 3 + b] = (a < D && b < D) ? A.R[a * D + b] : 0.0;
+            P[9 + a] = a < D ? A.t[a] : 0.0;
+        }
+    }
+    for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
+    int pairs = 0, list_rebuilds = 0, namb_total = 0;
+
+    // kCorrLoop: grid-stride over source tiles (waves never wait on each other until the final
+    // combine); otherwise one tile per wave
+#if GICP_CORR_LOOP
+    const int nwaves = gridDim.x * kCorrWaves;
+    for (int T = A.q_begin + blockIdx.x * kCorrWaves + w; T < A.q_end; T += nwaves) {
+#else
+    if (A.q_begin + blockIdx.x * kCorrWaves + w < A.q_end) {
+        const int T = A.q_begin + blockIdx.x * kCorrWaves + w;
+#endif
     bool on = false;          // accepted correspondence
     double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0;
     bool amb = false;
-    int pairs = 0;
-
-    if (active) {
+    {
         const TileInfo st = tile_meta(sc, T);
         Query<D> q;
         q.valid = l < st.count;
@@ -826,7 +900,8 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
         };
         float lb = lane_bound();   // refreshed after every merge
-        auto visit = [&](int Tt) -> bool {
+        // visit target tile Tt; `pre` = its coordinates already loaded (prefetch) or null
+        auto visit_pre = [&](int Tt, const float4* pre) -> bool {
             S.mark(1);
             const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
@@ -836,7 +911,8 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
                 return false;
             }
             const unsigned sub = sub_mask<D>(ti, pr, q.valid, lb);
-            stage_f32(tg, ti, L);
+            if (pre) stage_f32_from(*pre, L);
+            else stage_f32(tg, ti, L);
             S.mark(2);
             unsigned tb = 0xFFFFFFFFu, ts = 0xFFFFFFFFu;
             scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
@@ -856,8 +932,103 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             S.mark(3);
             return true;
         };
+        auto visit = [&](int Tt) -> bool { return visit_pre(Tt, nullptr); };
         S.mark(0);
-        traverse<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); });
+        // candidate list of this source tile: usable if built within the pose ring and the tile's
+        // displacement since then is inside the certified radius
+        bool use = false;
+        float delta = 0.f, rc = 0.f;
+        int nl = 0;
+        if (A.use_lists) {
+            nl = A.list_len[T];
+            rc = A.list_rcert[T];
+            const int bp = A.list_pass[T];
+            if (nl > 0 && rc > 0.f && A.pass - bp > 0 && A.pass - bp < kPoseRing) {
+                const double* Pb = A.poses + (bp % kPoseRing) * 12;
+                double dc2 = 0.0, dr2 = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    double m = A.t[a] - Pb[9 + a];
+#pragma unroll
+                    for (int b = 0; b < D; ++b) {
+                        const double dr = A.R[a * D + b] - Pb[a * 3 + b];
+                        m += dr * st.c[b];
+                        dr2 += dr * dr;
+                    }
+                    dc2 += m * m;
+                }
+                delta = (float)(sqrt(dc2) + sqrt(dr2) * (double)st.radius) * 1.0001f + 1e-30f;
+                use = delta < rc;
+            }
+        }
+        if (use) {
+            // lane k holds list entry k: its box gap to the wave box, start and count
+            int ent = 0, est = 0, ecnt = 0;
+            float eg2 = 3e38f;
+            if (l < nl) {
+                ent = A.list[(int64_t)T * kListMax + l];
+                eg2 = gap2_box<D>(q, tg.tiles[ent].c, tg.tiles[ent].h);
+                est = tg.tiles[ent].start;
+                ecnt = tg.tiles[ent].count;
+            }
+            float wb = wave_maxf(lb);
+            uint64_t rem = __ballot(l < nl && eg2 <= wb);
+            // nearest remaining entry (wave-uniform lane index), -1 if none
+            auto pick = [&]() -> int {
+                if (!rem) return -1;
+                const bool in = (rem >> l) & 1ull;
+                const float m = wave_minf(in ? eg2 : 3e38f);
+                const uint64_t c = __ballot(in && eg2 == m);
+                return __ffsll((unsigned long long)c) - 1;
+            };
+            int k = pick();
+            float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k >= 0) pv = load_rel(tg, __builtin_amdgcn_readlane(est, k), __builtin_amdgcn_readlane(ecnt, k));
+            while (k >= 0) {
+                rem &= ~(1ull << k);
+                const int kn = pick();   // prefetch the next-nearest while this one is scanned
+                float4 pvn = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (kn >= 0) pvn = load_rel(tg, __builtin_amdgcn_readlane(est, kn), __builtin_amdgcn_readlane(ecnt, kn));
+                if (visit_pre(__builtin_amdgcn_readlane(ent, k), &pv)) {
+                    wb = wave_maxf(lb);
+                    rem &= __ballot(eg2 <= wb);
+                }
+                if (kn >= 0 && ((rem >> kn) & 1ull)) {
+                    k = kn;
+                    pv = pvn;
+                } else {
+                    k = pick();
+                    if (k >= 0) pv = load_rel(tg, __builtin_amdgcn_readlane(est, k), __builtin_amdgcn_readlane(ecnt, k));
+                }
+            }
+            const float wbf = wave_maxf(lb);
+            if (__builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 1.0001f + delta > rc) {
+                // not certified: start over with the full walk (and rebuild the list)
+                use = false;
+                best = sec = init;
+                best_tile = -1;
+                lb = lane_bound();
+                ++list_rebuilds;
+            }
+        }
+        if (!use) {
+            int ncol = 0;
+            auto collect = [&](int Tt) {
+                if (ncol < kListMax && l == 0) A.list[(int64_t)T * kListMax + ncol] = Tt;
+                ++ncol;
+            };
+            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, A.use_lists ? A.skin : 0.f,
+                          collect);
+            if (A.use_lists) {
+                const float wbf = wave_maxf(lb);
+                const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + A.skin : 0.f;
+                if (l == 0) {
+                    A.list_len[T] = min(ncol, kListMax);
+                    A.list_rcert[T] = r;
+                    A.list_pass[T] = A.pass;
+                }
+            }
+        }
         S.mark(1);
 
         // the fp64 source point is needed only from here on (kept out of the walk's registers)
@@ -1057,25 +1228,28 @@ __global__ void __launch_bounds__(256) k_corr(CorrArgs A) {
             } else if (qq == NS + D && p <= NS + D + 1) {
                 idx = NS * NS + NS * D + NS + D * D + D + (p - NS - D);   // c0, count
             }
-            if (idx >= 0) s_wstat[w][idx] = acc[j];
+            if (idx >= 0) s_wstat[w][idx] += acc[j];   // each (p,q) has one owner lane: no race
         }
-        const int namb = (int)__popcll(__ballot(amb));
-        if (l == 0) {
-            s_wstat[w][NSS] = (double)namb;
-            s_wstat[w][NSS + 1] = (double)pairs * 64.0;
-        }
+        namb_total += (int)__popcll(__ballot(amb));
+    }
+    }   // tiles of this wave
+    if (l == 0) {
+        s_wstat[w][NSS] = (double)namb_total;
+        s_wstat[w][NSS + 1] = (double)pairs * 64.0;
+        s_wstat[w][NSS + 2] = (double)list_rebuilds;
     }
     S.mark(6);
 #ifdef GICP_STAMPS
+    S.acc[7] = (unsigned long long)pairs;   // slot 7: rows scanned (not cycles)
     if (A.stamps && l == 0)
-        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kWavesPerWG + w) * 8 + c] = S.acc[c];
+        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 8 + c] = S.acc[c];
 #endif
     __syncthreads();
-    if (threadIdx.x < NSX) {
+    for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) {
         double s = 0.0;
 #pragma unroll
-        for (int u = 0; u < kWavesPerWG; ++u) s += s_wstat[u][threadIdx.x];
-        A.partials[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;   // [statistic][workgroup]
+        for (int u = 0; u < kCorrWaves; ++u) s += s_wstat[u][t];
+        A.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;   // [statistic][workgroup]
     }
 }
 
@@ -1134,13 +1308,25 @@ hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
     return hipGetLastError();
 }
 
-int corr_grid(int q_tiles) { return (q_tiles + kWavesPerWG - 1) / kWavesPerWG; }
+// One resident generation of workgroups (occupancy x CUs), fewer if there are fewer tiles.
+int corr_grid(int q_tiles, int dim) {
+    static int cap[4] = {0, 0, 0, 0};
+    if (!cap[dim]) {
+        int dev = 0, ncu = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (dim == 2) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_corr<2>, 64 * kCorrWaves, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_corr<3>, 64 * kCorrWaves, 0);
+        cap[dim] = std::max(1, ncu) * std::max(1, per);
+    }
+    const int need = (q_tiles + kCorrWaves - 1) / kCorrWaves;
+    return kCorrLoop ? std::min(need, cap[dim]) : need;
+}
 
-hipError_t launch_corr(const CorrArgs& a, int dim, hipStream_t st) {
-    const int g = corr_grid(a.q_end - a.q_begin);
-    if (g <= 0) return hipSuccess;
-    if (dim == 2) hipLaunchKernelGGL(k_corr<2>, dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_corr<3>, dim3(g), dim3(256), 0, st, a);
+hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
+    if (grid <= 0) return hipSuccess;
+    if (dim == 2) hipLaunchKernelGGL(k_corr<2>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
+    else hipLaunchKernelGGL(k_corr<3>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
     return hipGetLastError();
 }
 

@@ -11,8 +11,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # GICP_LIB_VARIANT=stamps loads the diagnostic build with in-kernel phase timers (make STAMPS=1)
-LIB_PATH = os.path.join(HERE, "libgicp_hip_stamps.so" if os.environ.get("GICP_LIB_VARIANT") == "stamps"
-                        else "libgicp_hip.so")
+_VARIANT = os.environ.get("GICP_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, f"libgicp_hip_{_VARIANT}.so" if _VARIANT else "libgicp_hip.so")
 
 GICP_OK = 0
 GICP_E_INVALID = -1
