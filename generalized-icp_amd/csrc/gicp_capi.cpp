@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -29,7 +30,7 @@ hipError_t launch_build_tiles(const double*, int, const int32_t*, TileInfo*, int
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
-hipError_t launch_reduce(const double*, int, int, double*, hipStream_t);
+hipError_t launch_solve(IterState*, int, hipStream_t);
 int corr_grid(int, int);
 int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
 }  // namespace gicp
@@ -129,8 +130,11 @@ struct gicp_ctx {
     int32_t* d_hint = nullptr;
     double* d_partials = nullptr;
     size_t partials_cap = 0;
-    double* d_stats = nullptr;
-    double* h_stats = nullptr;
+    IterState* d_state = nullptr;
+    IterState* h_state = nullptr;     // pinned mirror
+    uint32_t* d_tickets = nullptr;
+    double* d_gpart = nullptr;
+    double h_stats[80];
     int32_t* d_amb = nullptr;
     int64_t* d_dbg_idx = nullptr;
     double* d_dbg_w = nullptr;
@@ -147,7 +151,8 @@ struct gicp_ctx {
     double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    static constexpr int kMaxBatch = 64;
+    hipEvent_t ev[2 * kMaxBatch] = {};
     // diagnostics of the last pass
     double last_amb = 0.0, last_pairs = 0.0;
     float last_corr_ms = 0.f, last_reduce_ms = 0.f;
@@ -378,35 +383,35 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
 
 void ensure_workspace(gicp_ctx* c) {
     const int nsx = nstat_ext(3);
-    const size_t need = (size_t)std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim)) * nsx;
+    const int grid = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim));
+    if ((grid + kGroupWG - 1) / kGroupWG > kMaxGroups) throw Fail{GICP_E_INVALID, "source shard too large"};
+    const size_t need = (size_t)grid * nsx;
     if (need > c->partials_cap) {
         dalloc(c->d_partials, need);
         c->partials_cap = need;
     }
-    if (!c->d_stats) dalloc(c->d_stats, nsx);
-    if (!c->h_stats) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_stats), sizeof(double) * nsx));
+    if (!c->d_state) {
+        dalloc(c->d_state, 1);
+        HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_state), sizeof(IterState)));
+        std::memset(c->h_state, 0, sizeof(IterState));
+        dalloc(c->d_tickets, kMaxGroups + 1);
+        HIPCHK(hipMemsetAsync(c->d_tickets, 0, sizeof(uint32_t) * (kMaxGroups + 1), c->stream));
+        dalloc(c->d_gpart, (size_t)kMaxGroups * nsx);
+    }
 }
 
-// One pass at pose T: statistics (all-reduced) into c->h_stats.
-void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
-    if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
-    if (c->tgt.dim != c->src.dim) throw Fail{GICP_E_INVALID, "source and target dimensions differ"};
-    const int d = c->src.dim, n1 = d + 1;
-    ensure_workspace(c);
+// kernel arguments of a pass (the pose comes from the device state)
+CorrArgs corr_args(gicp_ctx* c, int single_pass) {
+    const int d = c->src.dim;
     CorrArgs a{};
     a.src = c->src.view();
     a.tgt = c->tgt.view();
     a.q_begin = c->q_begin;
     a.q_end = c->q_end;
-    for (int r = 0; r < d; ++r) {
-        for (int k = 0; k < d; ++k) {
-            a.R[r * d + k] = T[r * n1 + k];
-            a.R32[r * d + k] = (float)T[r * n1 + k];
-        }
-        a.t[r] = T[r * n1 + d];
-    }
-    for (int k = 0; k < d * n1 + n1; ++k)
-        if (!std::isfinite(T[k])) throw Fail{GICP_E_INVALID, "pose contains non-finite values"};
+    a.state = c->d_state;
+    a.tickets = c->d_tickets;
+    a.gpart = c->d_gpart;
+    a.single_pass = single_pass;
     const double dc = c->psrc.max_distance_correspondence;
     a.dc = dc;
     a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc);
@@ -422,57 +427,18 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     a.pass = ++c->pass;
     a.use_lists = c->use_lists ? 1 : 0;
     a.skin = (float)(0.2 * dc);
-    if (dbg && (dbg->index || dbg->weight || dbg->distance)) {
-        const size_t n = (size_t)c->src.n;
-        if (c->dbg_cap < n) {
-            dalloc(c->d_dbg_idx, n);
-            dalloc(c->d_dbg_w, n * d * d);
-            dalloc(c->d_dbg_dist, n);
-            c->dbg_cap = n;
-        }
-        a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
-        a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
-        a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
-    }
-    const int nsx = nstat_ext(d);
-    const int grid = corr_grid(c->q_end - c->q_begin, d);
-    hipStream_t st = c->stream;
+    return a;
+}
+
+void allreduce_stats(gicp_ctx* c) {
+    if (!c->comm) return;
+    const int nsx = nstat_ext(c->src.dim);
+    ncclResult_t r = ncclAllReduce(c->d_state->stats, c->d_state->stats, nsx, ncclFloat64, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+}
+
 #ifdef GICP_STAMPS
-    static unsigned long long* d_stamps = nullptr;
-    static size_t stamps_cap = 0;
-    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 8;
-    if (nst > stamps_cap) {
-        dalloc(d_stamps, nst);
-        stamps_cap = nst;
-    }
-    HIPCHK(hipMemsetAsync(d_stamps, 0, nst * 8, st));
-    a.stamps = d_stamps;
-#endif
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], st));
-    if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], st));
-    if (grid > 0) HIPCHK(launch_reduce(c->d_partials, grid, nsx, c->d_stats, st));
-    else HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(double) * nsx, st));
-    if (c->comm) {
-        ncclResult_t r = ncclAllReduce(c->d_stats, c->d_stats, nsx, ncclFloat64, ncclSum, c->comm, st);
-        if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
-    }
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], st));
-    HIPCHK(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, st));
-    if (dbg) {
-        const size_t n = (size_t)c->src.n;
-        if (dbg->index) HIPCHK(hipMemcpyAsync(dbg->index, c->d_dbg_idx, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
-        if (dbg->weight)
-            HIPCHK(hipMemcpyAsync(dbg->weight, c->d_dbg_w, sizeof(double) * n * d * d, hipMemcpyDeviceToHost, st));
-        if (dbg->distance)
-            HIPCHK(hipMemcpyAsync(dbg->distance, c->d_dbg_dist, sizeof(double) * n, hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
-    if (c->timing) {
-        HIPCHK(hipEventElapsedTime(&c->last_corr_ms, c->ev[0], c->ev[1]));
-        HIPCHK(hipEventElapsedTime(&c->last_reduce_ms, c->ev[1], c->ev[2]));
-    }
-#ifdef GICP_STAMPS
+void print_stamps(const unsigned long long* d_stamps, size_t nst) {
     {
         std::vector<unsigned long long> hs(nst);
         HIPCHK(hipMemcpy(hs.data(), d_stamps, nst * 8, hipMemcpyDeviceToHost));
@@ -523,6 +489,64 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
         for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * tot[k] / std::max(1.0, all));
         std::fprintf(stderr, "\n");
     }
+}
+#endif
+
+// One pass at pose T: statistics (all-reduced) into c->h_stats.
+void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
+    if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
+    if (c->tgt.dim != c->src.dim) throw Fail{GICP_E_INVALID, "source and target dimensions differ"};
+    const int d = c->src.dim, n1 = d + 1;
+    for (int k = 0; k < n1 * n1; ++k)
+        if (!std::isfinite(T[k])) throw Fail{GICP_E_INVALID, "pose contains non-finite values"};
+    ensure_workspace(c);
+    hipStream_t st = c->stream;
+    IterState& hs = *c->h_state;
+    std::memset(&hs, 0, offsetof(IterState, stats));
+    for (int k = 0; k < n1 * n1; ++k) hs.T[k] = T[k];
+    hs.converged_at = -1;
+    HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
+    CorrArgs a = corr_args(c, 1);
+    if (dbg && (dbg->index || dbg->weight || dbg->distance)) {
+        const size_t n = (size_t)c->src.n;
+        if (c->dbg_cap < n) {
+            dalloc(c->d_dbg_idx, n);
+            dalloc(c->d_dbg_w, n * d * d);
+            dalloc(c->d_dbg_dist, n);
+            c->dbg_cap = n;
+        }
+        a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
+        a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
+        a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
+    }
+    const int nsx = nstat_ext(d);
+    const int grid = corr_grid(c->q_end - c->q_begin, d);
+#ifdef GICP_STAMPS
+    static unsigned long long* d_stamps = nullptr;
+    static size_t stamps_cap = 0;
+    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 8;
+    if (nst > stamps_cap) {
+        dalloc(d_stamps, nst);
+        stamps_cap = nst;
+    }
+    HIPCHK(hipMemsetAsync(d_stamps, 0, nst * 8, st));
+    a.stamps = d_stamps;
+#endif
+    if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
+    else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nsx, st));
+    allreduce_stats(c);
+    HIPCHK(hipMemcpyAsync(c->h_stats, c->d_state->stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, st));
+    if (dbg) {
+        const size_t n = (size_t)c->src.n;
+        if (dbg->index) HIPCHK(hipMemcpyAsync(dbg->index, c->d_dbg_idx, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+        if (dbg->weight)
+            HIPCHK(hipMemcpyAsync(dbg->weight, c->d_dbg_w, sizeof(double) * n * d * d, hipMemcpyDeviceToHost, st));
+        if (dbg->distance)
+            HIPCHK(hipMemcpyAsync(dbg->distance, c->d_dbg_dist, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+#ifdef GICP_STAMPS
+    print_stamps(d_stamps, nst);
 #endif
     const int ns = nstat(d);
     c->last_amb = c->h_stats[ns];
@@ -591,8 +615,8 @@ int gicp_create(gicp_ctx** out, int device) {
     }
     const int rc = guard_impl(c, "gicp_create", [&] {
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
         dalloc(c->d_amb, 4);
+        for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipMemsetAsync(c->d_amb, 0, sizeof(int32_t) * 4, c->stream));
     });
     if (rc != GICP_OK) {
@@ -612,7 +636,9 @@ void gicp_destroy(gicp_ctx* c) {
     c->src.release();
     dfree(c->d_hint);
     dfree(c->d_partials);
-    dfree(c->d_stats);
+    dfree(c->d_state);
+    dfree(c->d_tickets);
+    dfree(c->d_gpart);
     dfree(c->d_amb);
     dfree(c->d_dbg_idx);
     dfree(c->d_dbg_w);
@@ -622,7 +648,7 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_list_pass);
     dfree(c->d_list_rcert);
     dfree(c->d_poses);
-    if (c->h_stats) (void)hipHostFree(c->h_stats);
+    if (c->h_state) (void)hipHostFree(c->h_state);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -745,47 +771,74 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
     if (!c || !T_out) return GICP_E_INVALID;
     return guard_impl(c, "gicp_align", [&] {
         if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
+        if (c->tgt.dim != c->src.dim) throw Fail{GICP_E_INVALID, "source and target dimensions differ"};
         const int d = c->src.dim, n1 = d + 1;
         gicp_params prm = p ? resolve(d, p) : c->psrc;
         c->psrc.max_distance_correspondence = prm.max_distance_correspondence;
-        double T[16], Tn[16];
-        for (int k = 0; k < n1 * n1; ++k) T[k] = T0 ? T0[k] : ((k % (n1 + 1)) == 0 ? 1.0 : 0.0);
-        double last = INFINITY, loss = 0.0;
-        gicp_result r;
-        std::memset(&r, 0, sizeof(r));
-        r.converged_at = -1;
-        c->timing = res != nullptr;
+        ensure_workspace(c);
+        hipStream_t st = c->stream;
+        // device state: T0, last_loss = inf (gicp.py:106-110)
+        IterState& hs = *c->h_state;
+        std::memset(&hs, 0, offsetof(IterState, stats));
+        for (int k = 0; k < n1 * n1; ++k) hs.T[k] = T0 ? T0[k] : ((k % (n1 + 1)) == 0 ? 1.0 : 0.0);
+        for (int k = 0; k < n1 * n1; ++k)
+            if (!std::isfinite(hs.T[k])) throw Fail{GICP_E_INVALID, "T0 contains non-finite values"};
+        hs.last_loss = INFINITY;
+        hs.tol = prm.tolerance;
+        hs.fixed = prm.fixed_iterations ? 1 : 0;
+        hs.converged_at = -1;
+        HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
+        const int grid = corr_grid(c->q_end - c->q_begin, d);
+        const bool timing = res != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        double corr_ms = 0.0, red_ms = 0.0;
-        std::vector<double> st(nstat(d));
-        int it = 0;
-        for (; it < prm.max_iterations; ++it) {
-            run_pass(c, T, nullptr);
-            corr_ms += c->last_corr_ms;
-            red_ms += c->last_reduce_ms;
-            std::memcpy(st.data(), c->h_stats, sizeof(double) * st.size());
-            if (solve_pose(d, st.data(), T, Tn, &loss) != 0) throw Fail{GICP_E_INVALID, "pose solve failed"};
-            r.final_loss = loss;
-            r.correspondences = (int64_t)st[nstat(d) - 1];
-            if (!prm.fixed_iterations && std::fabs(last - loss) < prm.tolerance) {  // gicp.py:160-162
-                r.converged = 1;
-                r.converged_at = it;
-                ++it;
-                break;
+        double corr_ms = 0.0;
+        int enq = 0;
+        // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
+        // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
+        // After convergence the remaining launches of a batch exit at once.
+        while (enq < prm.max_iterations) {
+            const int B = std::min(prm.max_iterations - enq,
+                                   prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 4);
+            for (int b = 0; b < B; ++b) {
+                CorrArgs a = corr_args(c, 0);
+                if (timing) HIPCHK(hipEventRecord(c->ev[2 * b], st));
+                if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
+                else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nstat_ext(d), st));
+                if (timing) HIPCHK(hipEventRecord(c->ev[2 * b + 1], st));
+                allreduce_stats(c);
+                HIPCHK(launch_solve(c->d_state, d, st));
             }
-            last = loss;
-            std::memcpy(T, Tn, sizeof(double) * n1 * n1);
+            enq += B;
+            HIPCHK(hipMemcpyAsync(&hs, c->d_state, sizeof(IterState), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (timing)
+                for (int b = 0; b < B; ++b) {
+                    float ms = 0.f;
+                    HIPCHK(hipEventElapsedTime(&ms, c->ev[2 * b], c->ev[2 * b + 1]));
+                    corr_ms += ms;
+                }
+            if (hs.converged) break;
         }
         const auto t1 = std::chrono::steady_clock::now();
-        c->timing = false;
-        std::memcpy(T_out, T, sizeof(double) * n1 * n1);
-        r.iterations = it;
-        r.ambiguous = (int32_t)c->last_amb;
-        r.pairs_evaluated = (int64_t)c->last_pairs;
-        r.wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        r.corr_kernel_ms = corr_ms;
-        r.reduce_ms = red_ms;
-        if (res) *res = r;
+        if (hs.solve_fail) throw Fail{GICP_E_INVALID, "pose solve failed (degenerate statistics)"};
+        std::memcpy(T_out, hs.T, sizeof(double) * n1 * n1);
+        if (res) {
+            gicp_result r;
+            std::memset(&r, 0, sizeof(r));
+            const int ns = nstat(d);
+            r.iterations = hs.iter;
+            r.converged = hs.converged;
+            r.converged_at = hs.converged ? hs.converged_at : -1;
+            r.final_loss = hs.loss;
+            r.correspondences = (int64_t)hs.stats_solved[ns - 1];
+            r.ambiguous = (int32_t)hs.stats_solved[ns];
+            r.pairs_evaluated = (int64_t)hs.stats_solved[ns + 1];
+            r.wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+            // kernel time of the iterations actually executed (after convergence launches exit at once)
+            r.corr_kernel_ms = corr_ms;
+            r.reduce_ms = 0.0;
+            *res = r;
+        }
     });
 }
 

@@ -84,16 +84,38 @@ struct CovArgs {
     int32_t* amb_counter;     // diagnostics (may be null)
 };
 
+// Device-resident state of the outer loop (gicp.py:106-110,155-167): the pose every pass reads,
+// the convergence bookkeeping k_solve updates, and the last pass's statistics.
+struct IterState {
+    double T[16];             // current pose (d+1)^2 row-major (gicp.py:107,166)
+    double loss;              // min_loss of the last inner solve (gicp.py:154)
+    double last_loss;         // gicp.py:110,165
+    double tol;               // gicp.py:78 tolerance
+    int32_t converged;        // 1 once |last_loss - min_loss| < tolerance (gicp.py:160)
+    int32_t converged_at;     // iteration index of that test, -1 if none
+    int32_t iter;             // outer iterations executed
+    int32_t fixed;            // 1: never stop on tolerance (benchmark mode)
+    int32_t solve_fail;
+    int32_t pad;
+    double stats[80];         // statistics of the last pass (summed over ranks when a communicator is set)
+    double stats_solved[80];  // copy of the statistics the last k_solve consumed (reporting)
+};
+
+constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
+constexpr int kMaxGroups = 4096;   // ticket counters available
+
 struct CorrArgs {
     DevCloud src, tgt;
     int32_t q_begin, q_end;   // this rank's source tiles
-    double R[9], t[3];
-    float R32[9];
+    IterState* state;         // pose in, statistics out
+    uint32_t* tickets;        // [kMaxGroups + 1] arrival counters, zero between launches (self-resetting)
+    double* gpart;            // [kMaxGroups][nstat_ext] group partials
+    int32_t single_pass;      // 1: run even if state->converged (gicp_iterate)
     float search2;            // fp32 screen bound (d_c^2 + margins)
     double dc;                // d_c, fp64, inclusive (distance > d_c rejects)
     Margin mg;
     int32_t* hint;            // [src.ntiles] best target tile of the previous pass
-    double* partials;         // [gridDim.x][nstat_ext]
+    double* partials;         // [gridDim.x][nstat_ext] workgroup partials
     int64_t* dbg_index;       // [N] original order (nullable)
     double* dbg_weight;       // [N][dim][dim] (nullable)
     double* dbg_dist;         // [N] (nullable)

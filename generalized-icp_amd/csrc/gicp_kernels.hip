@@ -8,7 +8,7 @@
 //                  (exact 1-NN in the target, accept d <= d_c, W = inv(C_s + C_t)),
 //                  fused with the sufficient statistics of loss()/grad_loss()
 //                  (gicp.py:52-76) so the inner minimisation needs no further pass
-//   k_reduce    <- deterministic sum of the per-workgroup statistics
+//   k_solve     <- the inner solve + convergence test on the device (gicp.py:148-167)
 //
 // Design: one wave = one query tile of <= 64 Morton-coherent points.
 // Database tiles are culled with a two-level AABB hierarchy (blocks of 64 tiles, tested
@@ -23,6 +23,7 @@
 #include <utility>
 
 #include "gicp_internal.h"
+#include "gicp_solver.h"
 
 namespace gicp {
 
@@ -831,13 +832,31 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     const DevCloud& sc = A.src;
     const DevCloud& tg = A.tgt;
 
+    // pose of this pass from the device state (uniform, scalar loads); converged loops skip
+    typedef __attribute__((address_space(4))) const IterState* ConstState;
+    const ConstState cs0 = (ConstState)(uintptr_t)A.state;
+    if (cs0->converged && !A.single_pass) return;
+    struct {
+        double R[9], t[3];
+        float R32[9];
+    } P;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) {
+            P.R[a * D + b] = cs0->T[a * (D + 1) + b];
+            P.R32[a * D + b] = (float)P.R[a * D + b];
+        }
+        P.t[a] = cs0->T[a * (D + 1) + D];
+    }
+
     Stamps S;
     S.start();
     if (A.use_lists && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
-        double* P = A.poses + (A.pass % kPoseRing) * 12;
+        double* ring = A.poses + (A.pass % kPoseRing) * 12;
         for (int a = 0; a < 3; ++a) {
-            for (int b = 0; b < 3; ++b) P[a * 3 + b] = (a < D && b < D) ? A.R[a * D + b] : 0.0;
-            P[9 + a] = a < D ? A.t[a] : 0.0;
+            for (int b = 0; b < 3; ++b) ring[a * 3 + b] = (a < D && b < D) ? P.R[a * D + b] : 0.0;
+            ring[9 + a] = a < D ? P.t[a] : 0.0;
         }
     }
     for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
@@ -864,13 +883,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         const float relv[3] = {rel.x, rel.y, rel.z};
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            double o = A.t[a];
+            double o = P.t[a];
             float pw = 0.f, ew = 0.f;
 #pragma unroll
             for (int b = 0; b < D; ++b) {
-                o += A.R[a * D + b] * st.c[b];
-                pw = fmaf(A.R32[a * D + b], relv[b], pw);
-                ew = fmaf(fabsf(A.R32[a * D + b]), st.h[b], ew);
+                o += P.R[a * D + b] * st.c[b];
+                pw = fmaf(P.R32[a * D + b], relv[b], pw);
+                ew = fmaf(fabsf(P.R32[a * D + b]), st.h[b], ew);
             }
             q.ow[a] = o;
             q.pw[a] = pw;
@@ -948,10 +967,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 double dc2 = 0.0, dr2 = 0.0;
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
-                    double m = A.t[a] - Pb[9 + a];
+                    double m = P.t[a] - Pb[9 + a];
 #pragma unroll
                     for (int b = 0; b < D; ++b) {
-                        const double dr = A.R[a * D + b] - Pb[a * 3 + b];
+                        const double dr = P.R[a * D + b] - Pb[a * 3 + b];
                         m += dr * st.c[b];
                         dr2 += dr * dr;
                     }
@@ -1037,9 +1056,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
             const double s4v[3] = {s4.x, s4.y, s4.z};
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                double p = A.t[a];
+                double p = P.t[a];
 #pragma unroll
-                for (int b = 0; b < D; ++b) p += A.R[a * D + b] * s4v[b];
+                for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
                 q.p64[a] = p;
                 sv[a] = s4v[a];
             }
@@ -1108,7 +1127,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 for (int a = 0; a < D; ++a) {
                     mr[a] = 0.0;
 #pragma unroll
-                    for (int b = 0; b < D; ++b) mr[a] += A.R[a * D + b] * ms[b];
+                    for (int b = 0; b < D; ++b) mr[a] += P.R[a * D + b] * ms[b];
                 }
                 double S[D][D];
 #pragma unroll
@@ -1245,29 +1264,106 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 8 + c] = S.acc[c];
 #endif
     __syncthreads();
+    // ---- deterministic two-level reduction inside the launch ----------------
+    // Workgroup partials are stored write-through (sc1) and drained before one lane's agent-scope
+    // ticket add; the last arriver of each group of kGroupWG workgroups (told by the value its add
+    // returned) takes an agent acquire and sums the group in index order; the last group does the
+    // same over the groups and writes the statistics into the device state.  Tickets self-reset.
+    __shared__ int s_last;
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) {
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < kCorrWaves; ++u) s += s_wstat[u][t];
-        A.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;   // [statistic][workgroup]
+        __hip_atomic_store(&A.partials[(int64_t)blockIdx.x * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int ng = (int)((gridDim.x + kGroupWG - 1) / kGroupWG);
+    const int g = (int)(blockIdx.x / kGroupWG);
+    if (threadIdx.x == 0) {
+        const int gn = min(kGroupWG, (int)gridDim.x - g * kGroupWG);
+        s_last = __hip_atomic_fetch_add(&A.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // rows [b0, b1) of `src` ([row][NSX]) summed per statistic in row order: 3 threads per statistic,
+    // each with its loads all in flight before the first add, combined in fixed order through LDS
+    __shared__ double s_red[3][NSX];
+    auto sum_rows = [&](const double* src, int b0, int b1, double* dst_stat /* nullable: into s_red[0] */) {
+        constexpr int PART = 22;   // rows per thread per chunk (3 x 22 = 66 rows per chunk)
+        static_assert(NSX * 3 <= 64 * kCorrWaves, "3 threads per statistic");
+        const int tid = threadIdx.x, st = tid % NSX, part = tid / NSX;
+        double acc = 0.0;
+        for (int c0 = b0; c0 < b1; c0 += 3 * PART) {
+            if (part < 3) {
+                double v[PART];
+#pragma unroll
+                for (int k = 0; k < PART; ++k) {
+                    const int b = c0 + part * PART + k;
+                    v[k] = b < b1 ? __hip_atomic_load(&src[(int64_t)b * NSX + st], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0.0;
+                }
+                double sp = 0.0;
+#pragma unroll
+                for (int k = 0; k < PART; ++k) sp += v[k];
+                s_red[part][st] = sp;
+            }
+            __syncthreads();
+            if (tid < NSX) acc += (s_red[0][tid] + s_red[1][tid]) + s_red[2][tid];
+            __syncthreads();
+        }
+        if (tid < NSX) dst_stat[tid] = acc;
+    };
+    __shared__ double s_sum[NSX];
+    {
+        const int b0 = g * kGroupWG, b1 = min((int)gridDim.x, b0 + kGroupWG);
+        sum_rows(A.partials, b0, b1, s_sum);
+        if (threadIdx.x < NSX)
+            __hip_atomic_store(&A.gpart[(int64_t)g * NSX + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&A.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = __hip_atomic_fetch_add(&A.tickets[kMaxGroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)(ng - 1);
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    sum_rows(A.gpart, 0, ng, s_sum);
+    if (threadIdx.x < NSX) A.state->stats[threadIdx.x] = s_sum[threadIdx.x];
+    if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Deterministic sum of the per-workgroup partials ([statistic][workgroup]): one workgroup per statistic.
-__global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ partials, int nparts, int nsx,
-                                                 double* __restrict__ out) {
-    __shared__ double sh[256];
-    const int v = blockIdx.x;
-    const double* row = partials + (int64_t)v * nparts;
-    double s = 0.0;
-    for (int p = threadIdx.x; p < nparts; p += 256) s += row[p];
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-        __syncthreads();
+// One lane: the inner solve (gicp.py:148-154) from the pass's statistics, then the convergence
+// test and pose update of gicp.py:155-167, all on the device so iterations need no host sync.
+template <int D>
+__global__ void __launch_bounds__(64) k_solve(IterState* S) {
+    if (threadIdx.x != 0 || S->converged) return;
+    for (int k = 0; k < 80; ++k) S->stats_solved[k] = S->stats[k];
+    const SolveOut<D> r = solve_pose_t<D>(S->stats, S->T);
+    const int it = S->iter;
+    S->iter = it + 1;
+    if (!r.ok) S->solve_fail = 1;
+    S->loss = r.loss;
+    if (!S->fixed && fabs(S->last_loss - r.loss) < S->tol) {   // gicp.py:160: stop before the update
+        S->converged = 1;
+        S->converged_at = it;
+        return;
     }
-    if (threadIdx.x == 0) out[v] = sh[0];
+    S->last_loss = r.loss;
+#pragma unroll
+    for (int k = 0; k < (D + 1) * (D + 1); ++k) S->T[k] = r.T[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1330,8 +1426,9 @@ hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_reduce(const double* partials, int nparts, int nsx, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce, dim3(nsx), dim3(256), 0, st, partials, nparts, nsx, out);
+hipError_t launch_solve(IterState* st, int dim, hipStream_t stream) {
+    if (dim == 2) hipLaunchKernelGGL(k_solve<2>, dim3(1), dim3(64), 0, stream, st);
+    else hipLaunchKernelGGL(k_solve<3>, dim3(1), dim3(64), 0, stream, st);
     return hipGetLastError();
 }
 

@@ -1,0 +1,345 @@
+// gicp_solver.h — the inner solve of GICP from the reduced statistics, host AND device.
+//
+// Reference: gicp.py:148-154 minimises sum_i r_i^T W_i r_i, r_i = q_i - R s_i - t, with the
+// correspondences and weights of the iteration held fixed, starting at the previous optimum.
+// For fixed (q, W) that loss is exactly  f(z) = c0 - 2 g^T (z - z_k) + (z - z_k)^T H (z - z_k)
+// in z = (vec R row-major, t).  t is eliminated in closed form (Schur
+// complement) and the rotation is found by damped Newton on SO(d) from R_k.
+//
+// Written with fixed sizes and fully unrolled loops (no data-dependent indexing, Cholesky
+// instead of pivoting) so the same code runs on the host (gicp_solve_pose) and in one GPU
+// lane (the device-side loop of gicp_align) with every array in registers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gicp {
+
+#define GICP_HD __host__ __device__ __forceinline__
+
+template <int D>
+struct SolveOut {
+    double T[(D + 1) * (D + 1)];
+    double loss;
+    int ok;
+};
+
+namespace solver_detail {
+
+template <int D>
+GICP_HD constexpr int sym(int a, int b) {
+    return a <= b ? a * D - a * (a - 1) / 2 + (b - a) : b * D - b * (b - 1) / 2 + (a - b);
+}
+
+// Cholesky solve of an N x N SPD system (lower factor in place); returns false if not SPD.
+template <int N>
+GICP_HD bool chol(double (&M)[N][N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double s = M[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= M[j][k] * M[j][k];
+        if (!(s > 0.0)) return false;
+        const double r = sqrt(s);
+        M[j][j] = r;
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            double t = M[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= M[i][k] * M[j][k];
+            M[i][j] = t / r;
+        }
+    }
+    return true;
+}
+template <int N>
+GICP_HD void chol_solve(const double (&L)[N][N], const double (&b)[N], double (&x)[N]) {
+    double y[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double s = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+        y[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        double s = y[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) s -= L[k][i] * x[k];
+        x[i] = s / L[i][i];
+    }
+}
+
+// R <- exp([w]) R (left perturbation)
+template <int D>
+GICP_HD void rot_update(const double* w, const double (&R)[D * D], double (&Rn)[D * D]) {
+    if constexpr (D == 2) {
+        const double c = cos(w[0]), s = sin(w[0]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            Rn[b] = c * R[b] - s * R[2 + b];
+            Rn[2 + b] = s * R[b] + c * R[2 + b];
+        }
+    } else {
+        const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+        const double th = sqrt(th2);
+        double s1, s2;
+        if (th < 1e-8) {
+            s1 = 1.0 - th2 / 6.0;
+            s2 = 0.5 - th2 / 24.0;
+        } else {
+            s1 = sin(th) / th;
+            s2 = (1.0 - cos(th)) / th2;
+        }
+        const double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+        double E[9];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const double k2 = K[a * 3] * K[b] + K[a * 3 + 1] * K[3 + b] + K[a * 3 + 2] * K[6 + b];
+                E[a * 3 + b] = (a == b ? 1.0 : 0.0) + s1 * K[a * 3 + b] + s2 * k2;
+            }
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) Rn[a * 3 + b] = E[a * 3] * R[b] + E[a * 3 + 1] * R[3 + b] + E[a * 3 + 2] * R[6 + b];
+    }
+}
+
+// generator k of so(d) applied from the left: out = G_k R
+template <int D>
+GICP_HD void gen_mul(int k, const double (&R)[D * D], double (&out)[D * D]) {
+    if constexpr (D == 2) {
+        out[0] = -R[2];
+        out[1] = -R[3];
+        out[2] = R[0];
+        out[3] = R[1];
+    } else {
+        // G_k = [e_k]x ; rows: (G R)_a = sum_b G_ab R_b
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const double r0 = R[b], r1 = R[3 + b], r2 = R[6 + b];
+            if (k == 0) {
+                out[b] = 0.0;
+                out[3 + b] = -r2;
+                out[6 + b] = r1;
+            } else if (k == 1) {
+                out[b] = r2;
+                out[3 + b] = 0.0;
+                out[6 + b] = -r0;
+            } else {
+                out[b] = -r1;
+                out[3 + b] = r0;
+                out[6 + b] = 0.0;
+            }
+        }
+    }
+}
+
+}  // namespace solver_detail
+
+// Minimise the quadratic of `st` (layout DESIGN.md §4) over SE(D) from Tk.
+template <int D>
+GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
+    using namespace solver_detail;
+    constexpr int NS = D * (D + 1) / 2, NR = D * D, N1 = D + 1, M = D == 2 ? 1 : 3;
+    SolveOut<D> out;
+    out.ok = 1;
+#pragma unroll
+    for (int k = 0; k < N1 * N1; ++k) out.T[k] = Tk[k];
+    out.loss = 0.0;
+    const double* A = st;
+    const double* B = A + NS * NS;
+    const double* C = B + NS * D;
+    const double* gR = C + NS;
+    const double* gt = gR + D * D;
+    const double c0 = gt[D];
+    const double cnt = gt[D + 1];
+    if (!(cnt > 0.5)) return out;   // no correspondences: loss identically 0, pose unchanged
+
+    double Rk[NR], tk[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) Rk[a * D + b] = Tk[a * N1 + b];
+        tk[a] = Tk[a * N1 + D];
+    }
+    // Htt (Cholesky), K = Htt^-1 Htr, kt = Htt^-1 gt
+    double L[D][D];
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+        for (int b = 0; b < D; ++b) L[a][b] = C[sym<D>(a, b)];
+    if (!chol<D>(L)) {
+        out.ok = 0;
+        return out;
+    }
+    double kt[D], Kc[D][NR];
+    {
+        double rhs[D], x[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) rhs[a] = gt[a];
+        chol_solve<D>(L, rhs, x);
+#pragma unroll
+        for (int a = 0; a < D; ++a) kt[a] = x[a];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) {
+            const int ci = c / D, cj = c % D;   // column (ci, cj) of Htr: H[t_b][(ci,cj)] = B[sym(ci,b)][cj]
+#pragma unroll
+            for (int b = 0; b < D; ++b) rhs[b] = B[sym<D>(ci, b) * D + cj];
+            chol_solve<D>(L, rhs, x);
+#pragma unroll
+            for (int a = 0; a < D; ++a) Kc[a][c] = x[a];
+        }
+    }
+    // reduced quadratic in dr: c0' - 2 g'^T dr + dr^T H' dr
+    double Hp[NR][NR], gp[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const int ia = i / D, ii = i % D;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int jb = j / D, jj = j % D;
+            double s = A[sym<D>(ia, jb) * NS + sym<D>(ii, jj)];
+#pragma unroll
+            for (int a = 0; a < D; ++a) s -= B[sym<D>(ia, a) * D + ii] * Kc[a][j];
+            Hp[i][j] = s;
+        }
+        double s = gR[i];
+#pragma unroll
+        for (int a = 0; a < D; ++a) s -= B[sym<D>(ia, a) * D + ii] * kt[a];
+        gp[i] = s;
+    }
+    double c0p = c0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) c0p -= gt[a] * kt[a];
+
+    auto phi = [&](const double (&R)[NR]) {
+        double dr[NR], f = c0p;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) dr[i] = R[i] - Rk[i];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            double hi = 0.0;
+#pragma unroll
+            for (int j = 0; j < NR; ++j) hi += Hp[i][j] * dr[j];
+            f += dr[i] * hi - 2.0 * gp[i] * dr[i];
+        }
+        return f;
+    };
+
+    double R[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) R[i] = Rk[i];
+    double f = phi(R);
+    double lam = 0.0;
+    for (int it = 0; it < 100; ++it) {
+        double u[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            double s = -gp[i];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) s += Hp[i][j] * (R[j] - Rk[j]);
+            u[i] = s;   // H' dr - g'
+        }
+        double Dk[M][NR], grad[M], Hs[M][M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            gen_mul<D>(k, R, Dk[k]);
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < NR; ++i) s += u[i] * Dk[k][i];
+            grad[k] = 2.0 * s;
+        }
+#pragma unroll
+        for (int l = 0; l < M; ++l) {
+            double HD[NR];
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j) s += Hp[i][j] * Dk[l][j];
+                HD[i] = s;
+            }
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+                double s = 0.0;
+#pragma unroll
+                for (int i = 0; i < NR; ++i) s += Dk[k][i] * HD[i];
+                // second-order term: u . vec(1/2 (G_k G_l + G_l G_k) R)
+                double GkDl[NR], GlDk[NR];
+                gen_mul<D>(k, Dk[l], GkDl);
+                gen_mul<D>(l, Dk[k], GlDk);
+                double t2 = 0.0;
+#pragma unroll
+                for (int i = 0; i < NR; ++i) t2 += u[i] * 0.5 * (GkDl[i] + GlDk[i]);
+                Hs[k][l] = 2.0 * s + 2.0 * t2;
+            }
+        }
+        double gmax = 0.0, hscale = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            gmax = fmax(gmax, fabs(grad[k]));
+            hscale = fmax(hscale, fabs(Hs[k][k]));
+        }
+        if (gmax == 0.0) break;
+        bool stepped = false;
+        double wmax = 0.0;
+        for (int tries = 0; tries < 60; ++tries) {
+            double Hd[M][M], ng[M], w[M];
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+#pragma unroll
+                for (int l = 0; l < M; ++l) Hd[k][l] = Hs[k][l] + (k == l ? lam * (hscale + 1e-300) : 0.0);
+                ng[k] = -grad[k];
+            }
+            bool ok = chol<M>(Hd);
+            if (ok) {
+                chol_solve<M>(Hd, ng, w);
+                double dd = 0.0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
+                ok = dd < 0.0;
+            }
+            if (ok) {
+                double Rn[NR];
+                rot_update<D>(w, R, Rn);
+                const double fn = phi(Rn);
+                wmax = 0.0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
+                if (fn <= f || wmax < 1e-15) {
+                    if (fn <= f) {
+#pragma unroll
+                        for (int i = 0; i < NR; ++i) R[i] = Rn[i];
+                        f = fn;
+                    }
+                    stepped = true;
+                    lam = lam > 0.0 ? lam * 0.1 : 0.0;
+                    if (lam < 1e-12) lam = 0.0;
+                    break;
+                }
+            }
+            lam = lam == 0.0 ? 1e-9 : lam * 10.0;
+        }
+        if (!stepped || wmax < 1e-15) break;
+    }
+    // t from the eliminated block
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double s = kt[a];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) s -= Kc[a][c] * (R[c] - Rk[c]);
+        out.T[a * N1 + D] = tk[a] + s;
+#pragma unroll
+        for (int b = 0; b < D; ++b) out.T[a * N1 + b] = R[a * D + b];
+    }
+#pragma unroll
+    for (int b = 0; b < D; ++b) out.T[D * N1 + b] = 0.0;
+    out.T[D * N1 + D] = 1.0;
+    out.loss = f;
+    return out;
+}
+
+}  // namespace gicp
