@@ -1345,13 +1345,237 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane: the inner solve (gicp.py:148-154) from the pass's statistics, then the convergence
+// solve_pose_t (gicp_solver.h) restated for one wave: the reduced NR x NR Hessian H' is built and
+// held one row per lane (lane i < NR), so the matrix-vector products of the damped Newton loop
+// (H' dr, H' D_l, the loss) are lane-parallel and meet through LDS; the small dense work
+// (the M x M Newton system, the rotation update) runs redundantly in every lane, which keeps
+// the control flow uniform. Same iterates as the serial solver up to summation order.
+template <int D>
+__device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
+    using namespace solver_detail;
+    constexpr int NS = D * (D + 1) / 2, NR = D * D, N1 = D + 1, M = D == 2 ? 1 : 3;
+    __shared__ double s_kc[D][NR], s_u[NR], s_hd[M][NR], s_f[NR];
+    const int lane = threadIdx.x;
+    const int i = lane < NR ? lane : 0;   // lanes >= NR shadow row 0 and never store
+    SolveOut<D> out;
+    out.ok = 1;
+#pragma unroll
+    for (int k = 0; k < N1 * N1; ++k) out.T[k] = Tk[k];
+    out.loss = 0.0;
+    const double* A = st;
+    const double* B = A + NS * NS;
+    const double* C = B + NS * D;
+    const double* gR = C + NS;
+    const double* gt = gR + D * D;
+    const double c0 = gt[D];
+    if (!(gt[D + 1] > 0.5)) return out;
+
+    double Rk[NR], tk[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) Rk[a * D + b] = Tk[a * N1 + b];
+        tk[a] = Tk[a * N1 + D];
+    }
+    double L[D][D];
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+        for (int b = 0; b < D; ++b) L[a][b] = C[sym<D>(a, b)];
+    if (!chol<D>(L)) {
+        out.ok = 0;
+        return out;
+    }
+    double kt[D];
+    {
+        double rhs[D], x[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) rhs[a] = gt[a];
+        chol_solve<D>(L, rhs, kt);
+        // column i of K = Htt^-1 Htr on lane i
+        const int ci = i / D, cj = i % D;
+#pragma unroll
+        for (int b = 0; b < D; ++b) rhs[b] = B[sym<D>(ci, b) * D + cj];
+        chol_solve<D>(L, rhs, x);
+        if (lane < NR)
+#pragma unroll
+            for (int a = 0; a < D; ++a) s_kc[a][lane] = x[a];
+    }
+    __syncthreads();
+    // row i of H' and g'_i
+    double Hrow[NR], gpi;
+    {
+        const int ia = i / D, ii = i % D;
+        double bi[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) bi[a] = B[sym<D>(ia, a) * D + ii];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            double s = A[sym<D>(ia, j / D) * NS + sym<D>(ii, j % D)];
+#pragma unroll
+            for (int a = 0; a < D; ++a) s -= bi[a] * s_kc[a][j];
+            Hrow[j] = s;
+        }
+        gpi = gR[i];
+#pragma unroll
+        for (int a = 0; a < D; ++a) gpi -= bi[a] * kt[a];
+    }
+    double c0p = c0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) c0p -= gt[a] * kt[a];
+
+    // loss at R (phi of the serial solver) and, on lane i, u_i = (H' dr - g')_i
+    auto eval = [&](const double (&Rv)[NR], double& ui) {
+        double hi = 0.0, dri = 0.0;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const double dr = Rv[j] - Rk[j];
+            hi += Hrow[j] * dr;
+            dri = j == i ? dr : dri;
+        }
+        ui = hi - gpi;
+        if (lane < NR) s_f[lane] = dri * hi - 2.0 * gpi * dri;
+        __syncthreads();
+        double f = c0p;
+#pragma unroll
+        for (int j = 0; j < NR; ++j) f += s_f[j];
+        __syncthreads();
+        return f;
+    };
+
+    double R[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) R[k] = Rk[k];
+    double ui;
+    double f = eval(R, ui);
+    double lam = 0.0;
+    for (int it = 0; it < 100; ++it) {
+        double Dk[M][NR];
+#pragma unroll
+        for (int k = 0; k < M; ++k) gen_mul<D>(k, R, Dk[k]);
+        if (lane < NR) {
+            s_u[lane] = ui;
+#pragma unroll
+            for (int l = 0; l < M; ++l) {
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j) s += Hrow[j] * Dk[l][j];
+                s_hd[l][lane] = s;
+            }
+        }
+        __syncthreads();
+        // grad_k = 2 u.vec(G_k R) and the second-order term u.vec(1/2 (G_k G_l + G_l G_k) R) of the
+        // serial solver, through P = R U^T (U = u as a D x D matrix): u.vec(X R) = tr(X P),
+        // G_k G_l = e_l e_k^T - delta_kl I in 3-D and G^2 = -I in 2-D.
+        double P[D][D];
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                double s = 0.0;
+#pragma unroll
+                for (int c = 0; c < D; ++c) s += R[a * D + c] * s_u[b * D + c];
+                P[a][b] = s;
+            }
+        double grad[M], Hs[M][M];
+        if constexpr (D == 2) {
+            grad[0] = 2.0 * (P[0][1] - P[1][0]);
+        } else {
+            grad[0] = 2.0 * (P[1][2] - P[2][1]);
+            grad[1] = 2.0 * (P[2][0] - P[0][2]);
+            grad[2] = 2.0 * (P[0][1] - P[1][0]);
+        }
+        double trP = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) trP += P[a][a];
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+#pragma unroll
+            for (int l = k; l < M; ++l) {
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j) s += Dk[k][j] * s_hd[l][j];
+                const double t2 = D == 2 ? -trP : 0.5 * (P[k][l] + P[l][k]) - (k == l ? trP : 0.0);
+                Hs[k][l] = Hs[l][k] = 2.0 * s + 2.0 * t2;
+            }
+        __syncthreads();   // s_u / s_hd are rewritten next iteration
+        double gmax = 0.0, hscale = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            gmax = fmax(gmax, fabs(grad[k]));
+            hscale = fmax(hscale, fabs(Hs[k][k]));
+        }
+        if (gmax == 0.0) break;
+        bool stepped = false;
+        double wmax = 0.0;
+        for (int tries = 0; tries < 60; ++tries) {
+            double Hd[M][M], ng[M], w[M];
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+#pragma unroll
+                for (int l = 0; l < M; ++l) Hd[k][l] = Hs[k][l] + (k == l ? lam * (hscale + 1e-300) : 0.0);
+                ng[k] = -grad[k];
+            }
+            bool ok = chol<M>(Hd);
+            if (ok) {
+                chol_solve<M>(Hd, ng, w);
+                double dd = 0.0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
+                ok = dd < 0.0;
+            }
+            if (ok) {
+                double Rn[NR], un;
+                rot_update<D>(w, R, Rn);
+                const double fn = eval(Rn, un);
+                wmax = 0.0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
+                if (fn <= f || wmax < 1e-15) {
+                    if (fn <= f) {
+#pragma unroll
+                        for (int k = 0; k < NR; ++k) R[k] = Rn[k];
+                        f = fn;
+                        ui = un;
+                    }
+                    stepped = true;
+                    lam = lam > 0.0 ? lam * 0.1 : 0.0;
+                    if (lam < 1e-12) lam = 0.0;
+                    break;
+                }
+            }
+            lam = lam == 0.0 ? 1e-9 : lam * 10.0;
+        }
+        if (!stepped || wmax < 1e-15) break;
+    }
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double s = kt[a];
+#pragma unroll
+        for (int c = 0; c < NR; ++c) s -= s_kc[a][c] * (R[c] - Rk[c]);
+        out.T[a * N1 + D] = tk[a] + s;
+#pragma unroll
+        for (int b = 0; b < D; ++b) out.T[a * N1 + b] = R[a * D + b];
+    }
+#pragma unroll
+    for (int b = 0; b < D; ++b) out.T[D * N1 + b] = 0.0;
+    out.T[D * N1 + D] = 1.0;
+    out.loss = f;
+    return out;
+}
+
+// One wave: the inner solve (gicp.py:148-154) from the pass's statistics, then the convergence
 // test and pose update of gicp.py:155-167, all on the device so iterations need no host sync.
 template <int D>
 __global__ void __launch_bounds__(64) k_solve(IterState* S) {
-    if (threadIdx.x != 0 || S->converged) return;
-    for (int k = 0; k < 80; ++k) S->stats_solved[k] = S->stats[k];
-    const SolveOut<D> r = solve_pose_t<D>(S->stats, S->T);
+    if (S->converged) return;
+    const int lane = threadIdx.x;
+    constexpr int NSX = nstat_ext(D);
+    if (lane < NSX) S->stats_solved[lane] = S->stats[lane];
+    if (lane + 64 < NSX) S->stats_solved[lane + 64] = S->stats[lane + 64];
+    const SolveOut<D> r = solve_pose_wave<D>(S->stats, S->T);
+    __syncthreads();   // every lane has read S->T
+    if (lane != 0) return;
     const int it = S->iter;
     S->iter = it + 1;
     if (!r.ok) S->solve_fail = 1;

@@ -84,9 +84,11 @@ GICP_HD void rot_update(const double* w, const double (&R)[D * D], double (&Rn)[
         const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
         const double th = sqrt(th2);
         double s1, s2;
-        if (th < 1e-8) {
-            s1 = 1.0 - th2 / 6.0;
-            s2 = 0.5 - th2 / 24.0;
+        if (th < 0.25) {
+            // sin(th)/th and (1-cos th)/th^2 by their series: truncation < th^12/6e9 < 1e-17 here,
+            // and no libm sin/cos on the device's single-wave solve (the Newton steps are small)
+            s1 = 1.0 + th2 * (-1.0 / 6 + th2 * (1.0 / 120 + th2 * (-1.0 / 5040 + th2 * (1.0 / 362880 + th2 * (-1.0 / 39916800)))));
+            s2 = 0.5 + th2 * (-1.0 / 24 + th2 * (1.0 / 720 + th2 * (-1.0 / 40320 + th2 * (1.0 / 3628800 + th2 * (-1.0 / 479001600)))));
         } else {
             s1 = sin(th) / th;
             s2 = (1.0 - cos(th)) / th2;

@@ -184,6 +184,32 @@ def test_iterate_is_deterministic(eng, scene3d):
     assert np.array_equal(a, b)
 
 
+def test_device_solve_matches_host_solve(eng, scene3d):
+    """k_solve (one wave, lane-parallel Newton) reaches the same pose as the host solver on the
+    statistics of the same pass, for two successive iterations (2-D and 3-D)."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    T = np.eye(4)
+    for n in (1, 2):
+        p.max_iterations = n
+        Tdev, _ = eng.align(None, p)
+        st = eng.iterate(T)
+        T, loss = gicp.solve_pose(st, T)
+        np.testing.assert_allclose(Tdev, T, rtol=0, atol=1e-12)
+    fx = load("robot_p0_r90")
+    kw = kwargs(fx)
+    p2 = gicp.default_params(2, fixed_iterations=1, max_iterations=1,
+                             max_distance_correspondence=float(kw["max_distance_correspondence"]),
+                             max_distance_nearest_neighbors=float(kw["max_distance_nearest_neighbors"]))
+    eng.set_target(fx["target"], p2)
+    eng.set_source(fx["source"], p2)
+    Tdev, _ = eng.align(None, p2)
+    Th, _ = gicp.solve_pose(eng.iterate(np.eye(3)), np.eye(3))
+    np.testing.assert_allclose(Tdev, Th, rtol=0, atol=1e-11)
+
+
 # ----------------------------------------------------------------------------- edge cases
 def test_duplicates_and_ties_2d(eng):
     """Exact duplicate target points (ties) and a point on the d_c boundary."""
