@@ -438,57 +438,42 @@ void allreduce_stats(gicp_ctx* c) {
 }
 
 #ifdef GICP_STAMPS
+// Diagnostic build: per wave 8 phase-cycle slots (7 = rows scanned) + 8 event counters.
 void print_stamps(const unsigned long long* d_stamps, size_t nst) {
-    {
-        std::vector<unsigned long long> hs(nst);
-        HIPCHK(hipMemcpy(hs.data(), d_stamps, nst * 8, hipMemcpyDeviceToHost));
-        double tot[8] = {0}, all = 0;
-        int nw = 0;
-        for (size_t w = 0; w < nst / 8; ++w) {
-            unsigned long long r = 0;
-            for (int k = 0; k < 7; ++k) r += hs[w * 8 + k];
-            if (!r) continue;
-            ++nw;
-            for (int k = 0; k < 7; ++k) {
-                tot[k] += (double)hs[w * 8 + k];
-                all += (double)hs[w * 8 + k];
-            }
-        }
-        {   // slowest 1% of waves vs the rest: phase mix and rows scanned
-            std::vector<std::pair<double, size_t>> byc;
-            for (size_t w = 0; w < nst / 8; ++w) {
-                double r = 0;
-                for (int k = 0; k < 7; ++k) r += (double)hs[w * 8 + k];
-                if (r > 0) byc.push_back({r, w});
-            }
-            std::sort(byc.begin(), byc.end());
-            const size_t n1 = std::max<size_t>(1, byc.size() / 100);
-            double slow[8] = {0}, med[8] = {0};
-            for (size_t i = 0; i < n1; ++i)
-                for (int k = 0; k < 8; ++k) slow[k] += (double)hs[byc[byc.size() - 1 - i].second * 8 + k] / n1;
-            for (size_t i = byc.size() / 2 - n1 / 2, e = i + n1; i < e && i < byc.size(); ++i)
-                for (int k = 0; k < 8; ++k) med[k] += (double)hs[byc[i].second * 8 + k] / n1;
-            std::fprintf(stderr, "[stamps] slowest1%%: rows %.0f setup %.0f trav %.0f stage %.0f scan %.0f fb %.0f epi %.0f red %.0f | median: rows %.0f setup %.0f trav %.0f stage %.0f scan %.0f fb %.0f epi %.0f red %.0f\n",
-                         slow[7], slow[0], slow[1], slow[2], slow[3], slow[4], slow[5], slow[6], med[7], med[0], med[1],
-                         med[2], med[3], med[4], med[5], med[6]);
-        }
-        std::vector<double> per;
-        per.reserve(nst / 8);
-        for (size_t w = 0; w < nst / 8; ++w) {
-            unsigned long long r = 0;
-            for (int k = 0; k < 7; ++k) r += hs[w * 8 + k];
-            if (r) per.push_back((double)r);
-        }
-        std::sort(per.begin(), per.end());
-        if (!per.empty())
-            std::fprintf(stderr, "[stamps] wave cycles p50 %.0f p90 %.0f p99 %.0f p999 %.0f max %.0f\n",
-                         per[per.size() / 2], per[per.size() * 9 / 10], per[per.size() * 99 / 100],
-                         per[per.size() * 999 / 1000], per.back());
-        static const char* nm[8] = {"setup", "traverse", "need+stage", "scan", "fallback", "epilogue", "reduce", "-"};
-        std::fprintf(stderr, "[stamps] waves %d, mean cycles/wave %.0f:", nw, all / std::max(1, nw));
-        for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * tot[k] / std::max(1.0, all));
-        std::fprintf(stderr, "\n");
+    constexpr int W = 16;
+    std::vector<unsigned long long> hs(nst);
+    HIPCHK(hipMemcpy(hs.data(), d_stamps, nst * 8, hipMemcpyDeviceToHost));
+    std::vector<std::pair<double, size_t>> byc;
+    double tot[W] = {0}, all = 0;
+    for (size_t w = 0; w < nst / W; ++w) {
+        double r = 0;
+        for (int k = 0; k < 7; ++k) r += (double)hs[w * W + k];
+        if (r <= 0) continue;
+        byc.push_back({r, w});
+        all += r;
+        for (int k = 0; k < W; ++k) tot[k] += (double)hs[w * W + k];
     }
+    if (byc.empty()) return;
+    std::sort(byc.begin(), byc.end());
+    const size_t nw = byc.size(), n1 = std::max<size_t>(1, nw / 100);
+    static const char* nm[W] = {"setup", "trav", "stage", "scan", "fb", "epi", "red", "rows",
+                                "visits", "scanned", "chunks", "list", "listlen", "blktests", "candblk", "fbtiles"};
+    auto row = [&](const char* tag, size_t b, size_t e) {
+        double m[W] = {0};
+        for (size_t i = b; i < e; ++i)
+            for (int k = 0; k < W; ++k) m[k] += (double)hs[byc[i].second * W + k] / (double)(e - b);
+        std::fprintf(stderr, "[stamps] %-9s", tag);
+        for (int k = 0; k < W; ++k) std::fprintf(stderr, " %s %.6g", nm[k], m[k]);
+        std::fprintf(stderr, "\n");
+    };
+    row("all", 0, nw);
+    row("median1%", nw / 2 - n1 / 2, nw / 2 - n1 / 2 + n1);
+    row("slowest1%", nw - n1, nw);
+    std::fprintf(stderr, "[stamps] wave cycles p50 %.0f p90 %.0f p99 %.0f p999 %.0f max %.0f\n", byc[nw / 2].first,
+                 byc[nw * 9 / 10].first, byc[nw * 99 / 100].first, byc[nw * 999 / 1000].first, byc.back().first);
+    std::fprintf(stderr, "[stamps] waves %zu, mean cycles/wave %.0f:", nw, all / (double)nw);
+    for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s %.1f%%", nm[k], 100.0 * tot[k] / std::max(1.0, all));
+    std::fprintf(stderr, "\n");
 }
 #endif
 
@@ -524,7 +509,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
 #ifdef GICP_STAMPS
     static unsigned long long* d_stamps = nullptr;
     static size_t stamps_cap = 0;
-    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 8;
+    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 16;
     if (nst > stamps_cap) {
         dalloc(d_stamps, nst);
         stamps_cap = nst;

@@ -88,9 +88,14 @@ struct Stamps {
         acc[c] += t - last;
         last = t;
     }
+    // event counters: 0 tile visits, 1 tiles scanned, 2 chunks scanned, 3 list used, 4 list length,
+    // 5 traversal block tests, 6 traversal candidate blocks, 7 fp64 fallback tiles
+    unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void count(int k, unsigned v = 1) { cnt[k] += v; }
 #else
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void count(int, unsigned = 1) {}
 #endif
 };
 
@@ -279,9 +284,12 @@ __device__ __forceinline__ float gap2_box(const Query<D>& q, const double* c, co
 // With skin > 0 every tile whose box lies within sqrt(wb) + skin of the wave box is also passed
 // to collect(T) (wb as it stands when the tile is tested; wb only shrinks, so at the end the
 // collected set holds every tile within sqrt(wb_final) + skin).
-template <int D, class Visit, class WB, class Collect>
+struct NoCount {
+    __device__ __forceinline__ void count(int, unsigned = 1) {}
+};
+template <int D, class Visit, class WB, class Collect, class Cnt = NoCount>
 __device__ __forceinline__ void traverse_c(const DevCloud& db, const Query<D>& q, int seed, Visit&& visit,
-                                           WB&& wave_bound, float skin, Collect&& collect) {
+                                           WB&& wave_bound, float skin, Collect&& collect, Cnt* cnt = nullptr) {
     const int l = lane_id();
     auto infl = [&](float w) -> float {
         if (skin <= 0.f || w < 0.f) return w;
@@ -298,6 +306,7 @@ __device__ __forceinline__ void traverse_c(const DevCloud& db, const Query<D>& q
         }
     }
     for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
+        if (cnt) cnt->count(5);
         const int b = b0 + l;
         bool cb = false;
         if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wbi;
@@ -306,6 +315,7 @@ __device__ __forceinline__ void traverse_c(const DevCloud& db, const Query<D>& q
             const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
             bm &= bm - 1;
             const int first = db.blocks[bb].first, nt = db.blocks[bb].ntiles;
+            if (cnt) cnt->count(6);
             const int t = first + l;
             bool ct = false, cv = false;
             if (l < nt && t != seed) {
@@ -343,6 +353,7 @@ __device__ __forceinline__ void traverse(const DevCloud& db, const Query<D>& q, 
 struct WaveStage {
     float x[kTile], y[kTile], z[kTile];           // fp32 screen coordinates, SoA
     double x64[kTile], y64[kTile], z64[kTile];    // fp64 coordinates (covariance sums, fallback)
+    int32_t perm[kTile];                          // original indices (fallback tie-break)
 };
 // statistics transpose image: 16 points x 16 u-terms and 16 x 16 v-terms (XOR-swizzled 16-B chunks)
 struct WaveStat {
@@ -922,6 +933,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         // visit target tile Tt; `pre` = its coordinates already loaded (prefetch) or null
         auto visit_pre = [&](int Tt, const float4* pre) -> bool {
             S.mark(1);
+            S.count(0);
             const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
             const bool need = lane_gap2<D>(q, ti, pr) <= lb;
@@ -939,6 +951,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 tb = min(tb, key);
             }, sub);
             pairs += rows_scanned(sub, ti.count);
+            S.count(1);
+            S.count(2, __popc(sub));
             if (tb < best) {
                 sec = min(best, ts);
                 best = tb;
@@ -980,9 +994,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 use = delta < rc;
             }
         }
+        int ent = 0;   // lane k: list entry k (when the list is used)
         if (use) {
+            S.count(3);
+            S.count(4, nl);
             // lane k holds list entry k: its box gap to the wave box, start and count
-            int ent = 0, est = 0, ecnt = 0;
+            int est = 0, ecnt = 0;
             float eg2 = 3e38f;
             if (l < nl) {
                 ent = A.list[(int64_t)T * kListMax + l];
@@ -1037,7 +1054,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 ++ncol;
             };
             traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, A.use_lists ? A.skin : 0.f,
-                          collect);
+                          collect, &S);
             if (A.use_lists) {
                 const float wbf = wave_maxf(lb);
                 const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + A.skin : 0.f;
@@ -1089,22 +1106,39 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 float pr[D];
                 const bool need = amb && lane_gap2<D>(q, ti, pr) <= lim;
                 if (!__any(need)) return false;
+                S.count(7);
+                const unsigned sub = sub_mask<D>(ti, pr, amb, lim);
                 stage_f64(tg, ti, L);
-                for (int jj = 0; jj < ti.count; ++jj) {
-                    const double qq[3] = {L.t.x64[jj], L.t.y64[jj], L.t.z64[jj]};
-                    const double d2 = dist2_exact<D>(qq, q.p64);
-                    const int gj = ti.start + jj;
-                    const int og = tg.perm[gj];
-                    if (amb && (d2 < bd2 || (d2 == bd2 && og < bo))) {
-                        bd2 = d2;
-                        bj = gj;
-                        bo = og;
+                if (l < ti.count) L.t.perm[l] = tg.perm[ti.start + l];
+                wave_sync();
+                for (int g = 0; g < kSub; ++g) {
+                    if (!((sub >> g) & 1u)) continue;
+                    const int je = min(16 * g + 16, ti.count);
+#pragma unroll 4
+                    for (int jj = 16 * g; jj < je; ++jj) {
+                        const double qq[3] = {L.t.x64[jj], L.t.y64[jj], L.t.z64[jj]};
+                        const double d2 = dist2_exact<D>(qq, q.p64);
+                        const int og = L.t.perm[jj];
+                        if (amb && (d2 < bd2 || (d2 == bd2 && og < bo))) {
+                            bd2 = d2;
+                            bj = ti.start + jj;
+                            bo = og;
+                        }
                     }
                 }
                 wave_sync();
                 return true;
             };
-            traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
+            if (use) {   // the certified candidate list covers every tile within lb >= lim
+                uint64_t em = __ballot(l < nl);
+                while (em) {
+                    const int k = __ffsll((unsigned long long)em) - 1;
+                    em &= em - 1;
+                    visit64(__builtin_amdgcn_readlane(ent, k));
+                }
+            } else {
+                traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
+            }
             if (amb) j = bj;
         }
 
@@ -1260,8 +1294,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     S.mark(6);
 #ifdef GICP_STAMPS
     S.acc[7] = (unsigned long long)pairs;   // slot 7: rows scanned (not cycles)
-    if (A.stamps && l == 0)
-        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 8 + c] = S.acc[c];
+    if (A.stamps && l == 0) {
+        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 16 + c] = S.acc[c];
+        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 16 + 8 + c] = S.cnt[c];
+    }
 #endif
     __syncthreads();
     // ---- deterministic two-level reduction inside the launch ----------------
@@ -1293,39 +1329,49 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     // rows [b0, b1) of `src` ([row][NSX]) summed per statistic in row order: 3 threads per statistic,
     // each with its loads all in flight before the first add, combined in fixed order through LDS
     __shared__ double s_red[3][NSX];
-    auto sum_rows = [&](const double* src, int b0, int b1, double* dst_stat /* nullable: into s_red[0] */) {
-        constexpr int PART = 22;   // rows per thread per chunk (3 x 22 = 66 rows per chunk)
-        static_assert(NSX * 3 <= 64 * kCorrWaves, "3 threads per statistic");
-        const int tid = threadIdx.x, st = tid % NSX, part = tid / NSX;
-        double acc = 0.0;
-        for (int c0 = b0; c0 < b1; c0 += 3 * PART) {
-            if (part < 3) {
-                double v[PART];
+    auto sum_rows = [&](const double* src, int b0, int b1, double* dst_stat) {
+        constexpr int PART = 22;                                  // rows per thread per chunk
+        constexpr int NP = (64 * kCorrWaves) / NSX >= 3 ? 3 : 1;  // threads per statistic
+        constexpr int NT = 64 * kCorrWaves;
+        const int tid = threadIdx.x;
+        for (int s0 = 0; s0 < NSX; s0 += NT / NP) {   // statistics handled in this sweep
+            const int st = s0 + tid % (NT / NP), part = tid / (NT / NP);
+            const bool act = part < NP && st < NSX && tid % (NT / NP) < NSX;
+            double acc = 0.0;
+            for (int c0 = b0; c0 < b1; c0 += NP * PART) {
+                if (act) {
+                    double v[PART];
 #pragma unroll
-                for (int k = 0; k < PART; ++k) {
-                    const int b = c0 + part * PART + k;
-                    v[k] = b < b1 ? __hip_atomic_load(&src[(int64_t)b * NSX + st], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0.0;
+                    for (int k = 0; k < PART; ++k) {
+                        const int b = c0 + part * PART + k;
+                        v[k] = b < b1 ? __hip_atomic_load(&src[(int64_t)b * NSX + st], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0.0;
+                    }
+                    double sp = 0.0;
+#pragma unroll
+                    for (int k = 0; k < PART; ++k) sp += v[k];
+                    s_red[part][st] = sp;
                 }
-                double sp = 0.0;
+                __syncthreads();
+                if (act && part == 0) {
+                    double t = s_red[0][st];
 #pragma unroll
-                for (int k = 0; k < PART; ++k) sp += v[k];
-                s_red[part][st] = sp;
+                    for (int k = 1; k < NP; ++k) t += s_red[k][st];
+                    acc += t;
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            if (tid < NSX) acc += (s_red[0][tid] + s_red[1][tid]) + s_red[2][tid];
-            __syncthreads();
+            if (act && part == 0) dst_stat[st] = acc;
         }
-        if (tid < NSX) dst_stat[tid] = acc;
+        __syncthreads();
     };
     __shared__ double s_sum[NSX];
     {
         const int b0 = g * kGroupWG, b1 = min((int)gridDim.x, b0 + kGroupWG);
         sum_rows(A.partials, b0, b1, s_sum);
-        if (threadIdx.x < NSX)
-            __hip_atomic_store(&A.gpart[(int64_t)g * NSX + threadIdx.x], s_sum[threadIdx.x], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves)
+            __hip_atomic_store(&A.gpart[(int64_t)g * NSX + t], s_sum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1341,7 +1387,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     __syncthreads();
     if (!s_last) return;
     sum_rows(A.gpart, 0, ng, s_sum);
-    if (threadIdx.x < NSX) A.state->stats[threadIdx.x] = s_sum[threadIdx.x];
+    for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
