@@ -69,7 +69,7 @@ void dfree(T*& p) {
 struct Cloud {
     int dim = 0;
     int64_t n = 0;
-    int ntiles = 0, nblocks = 0, level = 0, bits = 0;
+    int ntiles = 0, nblocks = 0, level = 0, bits = 0;   // level: tile extent cap (grid cells)
     double lo[3] = {0, 0, 0};
     double scale = 1.0;
     float rho = 0.f;
@@ -146,8 +146,11 @@ struct gicp_ctx {
     int32_t* d_list_pass = nullptr;
     float* d_list_rcert = nullptr;
     double* d_poses = nullptr;
+    int32_t* d_order = nullptr;       // longest-first unit order (CorrArgs::order)
+    int32_t* d_order_cnt = nullptr;
     int pass = 0;
     bool use_lists = true;
+    bool use_order = true;            // GICP_NO_ORDER=1: identity workgroup order
     double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -200,43 +203,82 @@ float screen_bound(const Margin& m, double d) {
     return (float)(b * (1.0 + 1e-6)) + 1e-30f;
 }
 
-// Choose the finest Morton level whose cell-bounded tiles stay <= 1.3x the minimum count.
+// Cut the Morton-sorted points into tiles: runs of <= 64 consecutive points whose bounding box (in
+// Morton grid cells) stays within an extent cap E.  E is the smallest cap (steps of 2^(1/4)) whose
+// tile count stays <= 1.35x the minimum ceil(n/64): tiles are as compact as that budget allows, and
+// the cap bounds the largest tile, which sets both the widest query wave and the loosest box.
 void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
-                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& level_out) {
+                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out) {
     const int64_t n = (int64_t)codes.size();
-    const double target = 1.3 * std::ceil(n / 64.0) + 2.0;
-    int level = 0;
-    for (int lv = bits; lv >= 0; --lv) {
-        const int shift = dim * (bits - lv);
-        int64_t nt = 0, run = 1;
-        for (int64_t i = 1; i <= n; ++i) {
-            if (i == n || (shift >= 32 ? 0u : (codes[i] >> shift)) != (shift >= 32 ? 0u : (codes[i - 1] >> shift))) {
-                nt += (run + 63) / 64;
-                run = 1;
+    const int64_t target = (int64_t)(1.35 * std::ceil(n / 64.0)) + 2;
+    // decode the grid coordinates once
+    auto compact3 = [](uint32_t x) {   // inverse of the kernels' spread3
+        x &= 0x09249249u;
+        x = (x | (x >> 2)) & 0x030C30C3u;
+        x = (x | (x >> 4)) & 0x0300F00Fu;
+        x = (x | (x >> 8)) & 0x030000FFu;
+        x = (x | (x >> 16)) & 0x000003FFu;
+        return x;
+    };
+    auto compact2 = [](uint32_t x) {
+        x &= 0x55555555u;
+        x = (x | (x >> 1)) & 0x33333333u;
+        x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+        x = (x | (x >> 4)) & 0x00FF00FFu;
+        x = (x | (x >> 8)) & 0x0000FFFFu;
+        return x;
+    };
+    std::vector<uint16_t> g((size_t)n * dim);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t c = codes[i];
+        for (int a = 0; a < dim; ++a)
+            g[(size_t)i * dim + a] = (uint16_t)(dim == 3 ? compact3(c >> a) : compact2(c >> a));
+    }
+    auto cut = [&](int E, bool emit) -> int64_t {
+        int64_t nt = 0, i0 = 0;
+        int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+        for (int64_t i = 0; i <= n; ++i) {
+            bool brk = i == n || i - i0 == 64;
+            if (!brk && i > i0) {
+                for (int a = 0; a < dim; ++a) {
+                    const int v = g[(size_t)i * dim + a];
+                    if (std::max(hi[a], v) - std::min(lo[a], v) > E) brk = true;
+                }
+            }
+            if (brk && i > i0) {
+                ++nt;
+                if (emit) {
+                    start.push_back((int32_t)i0);
+                    count.push_back((int32_t)(i - i0));
+                    first_code.push_back(codes[i0]);
+                }
+                i0 = i;
+            }
+            if (i == n) break;
+            if (i == i0) {
+                for (int a = 0; a < dim; ++a) lo[a] = hi[a] = g[(size_t)i * dim + a];
             } else {
-                ++run;
+                for (int a = 0; a < dim; ++a) {
+                    lo[a] = std::min(lo[a], (int)g[(size_t)i * dim + a]);
+                    hi[a] = std::max(hi[a], (int)g[(size_t)i * dim + a]);
+                }
             }
         }
-        if (nt <= target) {
-            level = lv;
+        return nt;
+    };
+    const int emax = (1 << bits);
+    int E = emax;
+    for (double e = 2.0; e < emax; e *= 1.189207115) {   // 2^(1/4)
+        if (cut((int)e, false) <= target) {
+            E = (int)e;
             break;
         }
     }
-    level_out = level;
-    const int shift = dim * (bits - level);
     start.clear();
     count.clear();
     first_code.clear();
-    int64_t i0 = 0;
-    for (int64_t i = 1; i <= n; ++i) {
-        const bool brk = i == n || (shift >= 32 ? false : (codes[i] >> shift) != (codes[i - 1] >> shift));
-        if (brk || i - i0 == 64) {
-            start.push_back((int32_t)i0);
-            count.push_back((int32_t)(i - i0));
-            first_code.push_back(codes[i0]);
-            i0 = i;
-        }
-    }
+    cut(E, true);
+    cap_out = E;
 }
 
 // Build the device index of a cloud and its per-point covariances for tiles [qb, qe) (qe < 0: all).
@@ -318,6 +360,10 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         HIPCHK(hipMemcpyAsync(&rho_bits, d_rho, sizeof(unsigned), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         std::memcpy(&cl.rho, &rho_bits, sizeof(float));
+        if (const char* e = std::getenv("GICP_VERBOSE"))
+            if (e[0] == '1')
+                std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f\n",
+                             (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho);
 
         // surface covariances (gicp.py:19-35) for this rank's query tiles
         int qb = 0, qe = cl.ntiles;
@@ -362,6 +408,18 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     (void)hipFree(d_tmp);
 }
 
+// Per-source-tile state that refers to target tiles (hints, candidate lists, heavy schedule):
+// reset whenever either cloud changes.
+void reset_tile_state(gicp_ctx* c) {
+    const int nt = std::max(1, c->src.ntiles);
+    if (!c->d_hint) return;
+    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * nt, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_order_cnt, 0, sizeof(int32_t) * 2 * 8 * kOrderBuckets, c->stream));
+    c->pass = 0;
+}
+
 void set_shard(gicp_ctx* c, int shard, int nshards) {
     if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
     c->shard = shard;
@@ -370,15 +428,15 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     c->q_end = (int)((int64_t)c->src.ntiles * (shard + 1) / nshards);
     const int nt = std::max(1, c->src.ntiles);
     dalloc(c->d_hint, nt);
-    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * nt, c->stream));
     dalloc(c->d_list, (size_t)nt * kListMax);
     dalloc(c->d_list_len, nt);
     dalloc(c->d_list_pass, nt);
     dalloc(c->d_list_rcert, nt);
     if (!c->d_poses) dalloc(c->d_poses, (size_t)kPoseRing * 12);
-    HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
-    c->pass = 0;
+    const int q8 = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim) / 8);
+    dalloc(c->d_order, (size_t)2 * 8 * kOrderBuckets * q8);
+    if (!c->d_order_cnt) dalloc(c->d_order_cnt, 2 * 8 * kOrderBuckets);
+    reset_tile_state(c);
 }
 
 void ensure_workspace(gicp_ctx* c) {
@@ -417,6 +475,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc);
     a.search2 = screen_bound(a.mg, dc);
     a.hint = c->d_hint;
+    a.order = c->use_order ? c->d_order : nullptr;
+    a.order_cnt = c->d_order_cnt;
     a.partials = c->d_partials;
     a.count_pairs = 1;
     a.list = c->d_list;
@@ -440,9 +500,17 @@ void allreduce_stats(gicp_ctx* c) {
 #ifdef GICP_STAMPS
 // Diagnostic build: per wave 8 phase-cycle slots (7 = rows scanned) + 8 event counters.
 void print_stamps(const unsigned long long* d_stamps, size_t nst) {
-    constexpr int W = 16;
+    constexpr int W = 20;
     std::vector<unsigned long long> hs(nst);
     HIPCHK(hipMemcpy(hs.data(), d_stamps, nst * 8, hipMemcpyDeviceToHost));
+    if (const char* f = std::getenv("GICP_STAMPS_DUMP")) {   // raw [waves][20] u64 for offline analysis
+        static int seq = 0;
+        const std::string path = std::string(f) + "." + std::to_string(seq++);
+        if (FILE* fp = std::fopen(path.c_str(), "wb")) {
+            std::fwrite(hs.data(), 8, hs.size(), fp);
+            std::fclose(fp);
+        }
+    }
     std::vector<std::pair<double, size_t>> byc;
     double tot[W] = {0}, all = 0;
     for (size_t w = 0; w < nst / W; ++w) {
@@ -457,18 +525,24 @@ void print_stamps(const unsigned long long* d_stamps, size_t nst) {
     std::sort(byc.begin(), byc.end());
     const size_t nw = byc.size(), n1 = std::max<size_t>(1, nw / 100);
     static const char* nm[W] = {"setup", "trav", "stage", "scan", "fb", "epi", "red", "rows",
-                                "visits", "scanned", "chunks", "list", "listlen", "blktests", "candblk", "fbtiles"};
+                                "visits", "scanned", "chunks", "list", "listlen", "blktests", "candblk", "fbtiles",
+                                "t0", "t1", "hwid", "xcc"};
     auto row = [&](const char* tag, size_t b, size_t e) {
         double m[W] = {0};
         for (size_t i = b; i < e; ++i)
             for (int k = 0; k < W; ++k) m[k] += (double)hs[byc[i].second * W + k] / (double)(e - b);
         std::fprintf(stderr, "[stamps] %-9s", tag);
-        for (int k = 0; k < W; ++k) std::fprintf(stderr, " %s %.6g", nm[k], m[k]);
+        for (int k = 0; k < 16; ++k) std::fprintf(stderr, " %s %.6g", nm[k], m[k]);
         std::fprintf(stderr, "\n");
     };
     row("all", 0, nw);
     row("median1%", nw / 2 - n1 / 2, nw / 2 - n1 / 2 + n1);
     row("slowest1%", nw - n1, nw);
+    for (size_t i = nw - std::min<size_t>(nw, 4); i < nw; ++i) {
+        char tag[32];
+        std::snprintf(tag, sizeof tag, "w%zu", byc[i].second);
+        row(tag, i, i + 1);
+    }
     std::fprintf(stderr, "[stamps] wave cycles p50 %.0f p90 %.0f p99 %.0f p999 %.0f max %.0f\n", byc[nw / 2].first,
                  byc[nw * 9 / 10].first, byc[nw * 99 / 100].first, byc[nw * 999 / 1000].first, byc.back().first);
     std::fprintf(stderr, "[stamps] waves %zu, mean cycles/wave %.0f:", nw, all / (double)nw);
@@ -509,7 +583,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
 #ifdef GICP_STAMPS
     static unsigned long long* d_stamps = nullptr;
     static size_t stamps_cap = 0;
-    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 16;
+    const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 20;
     if (nst > stamps_cap) {
         dalloc(d_stamps, nst);
         stamps_cap = nst;
@@ -589,6 +663,7 @@ int gicp_create(gicp_ctx** out, int device) {
     if (!c) return GICP_E_NOMEM;
     c->device = device;
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_NO_ORDER")) c->use_order = !(e[0] == '1');
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;
@@ -633,6 +708,8 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_list_pass);
     dfree(c->d_list_rcert);
     dfree(c->d_poses);
+    dfree(c->d_order);
+    dfree(c->d_order_cnt);
     if (c->h_state) (void)hipHostFree(c->h_state);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -673,7 +750,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, 0, 1, true);
-        if (c->src.n) HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * std::max(1, c->src.ntiles), c->stream));
+        if (c->src.n) reset_tile_state(c);
     });
 }
 

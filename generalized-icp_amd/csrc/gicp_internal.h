@@ -19,15 +19,12 @@ constexpr int kWavesPerWG = 4;     // 256-thread workgroups, each wave independe
 #ifndef GICP_CORR_WAVES
 #define GICP_CORR_WAVES 4
 #endif
-#ifndef GICP_CORR_LOOP
-#define GICP_CORR_LOOP 0
-#endif
 constexpr int kCorrWaves = GICP_CORR_WAVES;       // waves per k_corr workgroup
-constexpr bool kCorrLoop = GICP_CORR_LOOP != 0;   // grid-stride over source tiles
 
 constexpr int kListMax = 64;       // candidate target tiles kept per source tile
 constexpr int kPoseRing = 64;      // passes a list stays usable for
 constexpr int kSub = 4;            // 16-row sub-tiles per tile (finer culling of the row scan)
+constexpr int kOrderBuckets = 16;  // cost classes of the longest-first workgroup order
 
 struct __attribute__((aligned(16))) TileInfo {
     double c[3];      // fp64 centre (midpoint of the fp64 AABB)
@@ -131,7 +128,15 @@ struct CorrArgs {
     int32_t pass;             // this pass's id (monotonic per source cloud)
     int32_t use_lists;        // 0: always full walk (no lists)
     float skin;
-    unsigned long long* stamps;  // [waves][8] phase cycles (STAMPS diagnostic build only; else null)
+    unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
+    // longest-first order: a UNIT is the kCorrWaves consecutive source tiles one
+    // workgroup handles; its partial row and reduction group follow the unit, so the statistics do
+    // not depend on the order.  Units 0 .. 8 q8 - 1 (q8 = units / 8) form 8 contiguous ranges, one
+    // per XCD; within a range the units run in decreasing cost class of the previous pass.
+    // order_cnt[parity][xcd][class], order[parity][xcd][class][q8]; parity = pass & 1 is read,
+    // the other parity is appended to at each workgroup's end (and zeroed after the next pass).
+    int32_t* order;           // null: identity order
+    int32_t* order_cnt;
 };
 
 constexpr int nstat(int D) {

@@ -81,8 +81,11 @@ __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 struct Stamps {
 #ifdef GICP_STAMPS
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long last = 0;
-    __device__ __forceinline__ void start() { last = __builtin_amdgcn_s_memtime(); }
+    unsigned long long last = 0, rt0 = 0;
+    __device__ __forceinline__ void start() {
+        last = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
     __device__ __forceinline__ void mark(int c) {
         const unsigned long long t = __builtin_amdgcn_s_memtime();
         acc[c] += t - last;
@@ -799,6 +802,16 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 // ---------------------------------------------------------------------------
 // per-iteration correspondences + weights + statistics
 // ---------------------------------------------------------------------------
+// Register budget of k_corr: on gfx950 a wave with next_free_sgpr >= 94 leaves 6 waves per SIMD,
+// <= 90 leaves 7 and <= 72 (with <= 64 VGPRs) 8 (scripts/probes/occupancy.hip measures it; the
+// compiler's own occupancy estimate does not model it).
+#ifndef GICP_CORR_ATTR
+#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR)))
+#endif
+#ifndef GICP_CORR_SGPR
+#define GICP_CORR_SGPR 88
+#endif
+
 template <int D>
 struct StatIdx {
     static constexpr int NS = D * (D + 1) / 2;
@@ -832,7 +845,7 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 }
 
 template <int D>
-__global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
+__global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
     constexpr int NSS = nstat(D);
     __shared__ WaveLds s_lds[kCorrWaves];
@@ -873,15 +886,33 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
     int pairs = 0, list_rebuilds = 0, namb_total = 0;
 
-    // kCorrLoop: grid-stride over source tiles (waves never wait on each other until the final
-    // combine); otherwise one tile per wave
-#if GICP_CORR_LOOP
-    const int nwaves = gridDim.x * kCorrWaves;
-    for (int T = A.q_begin + blockIdx.x * kCorrWaves + w; T < A.q_end; T += nwaves) {
-#else
-    if (A.q_begin + blockIdx.x * kCorrWaves + w < A.q_end) {
-        const int T = A.q_begin + blockIdx.x * kCorrWaves + w;
-#endif
+    // workgroup -> unit (kCorrWaves consecutive source tiles).  Workgroup b runs on XCD b % 8: the
+    // first 8 q8 workgroups are striped so that XCD x walks the contiguous unit range [x q8, x q8 + q8)
+    // (its L2 then holds that region of the target), longest-first within the range by the cost
+    // classes the previous pass recorded; the remaining units run in index order.
+    const int nunits = (int)gridDim.x, q8 = nunits / 8;
+    int unit = (int)blockIdx.x;
+    if (unit < 8 * q8) {
+        const int x = unit & 7, r = unit >> 3;
+        unit = x * q8 + r;
+        if (A.order) {
+            const int par = A.pass & 1;
+            const int32_t* cnt = A.order_cnt + (par * 8 + x) * kOrderBuckets;
+            int tot = 0;
+#pragma unroll
+            for (int k = 0; k < kOrderBuckets; ++k) tot += cnt[k];
+            if (tot == q8) {
+                int rr = r, k = kOrderBuckets - 1;
+                while (k > 0 && rr >= cnt[k]) rr -= cnt[k--];
+                unit = A.order[((int64_t)(par * 8 + x) * kOrderBuckets + k) * q8 + rr];
+            }
+        }
+    }
+    unit = __builtin_amdgcn_readfirstlane(unit);
+    const unsigned long long wg_t0 = __builtin_amdgcn_s_memtime();
+    int T = A.q_begin + unit * kCorrWaves + w;
+    if (T >= A.q_end) T = -1;
+    if (T >= 0) {
     bool on = false;          // accepted correspondence
     double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0;
     bool amb = false;
@@ -906,6 +937,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
             q.pw[a] = pw;
             q.ew[a] = ew * (1.0f + 4.8e-7f) + 1e-30f;
         }
+        const bool lists = A.use_lists != 0;
 
         // seed: last pass's best target tile for this source tile, else the Morton neighbour
         int seed = A.hint ? A.hint[T] : -1;
@@ -972,7 +1004,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         bool use = false;
         float delta = 0.f, rc = 0.f;
         int nl = 0;
-        if (A.use_lists) {
+        if (lists) {
             nl = A.list_len[T];
             rc = A.list_rcert[T];
             const int bp = A.list_pass[T];
@@ -1053,9 +1085,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
                 if (ncol < kListMax && l == 0) A.list[(int64_t)T * kListMax + ncol] = Tt;
                 ++ncol;
             };
-            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, A.use_lists ? A.skin : 0.f,
+            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, lists ? A.skin : 0.f,
                           collect, &S);
-            if (A.use_lists) {
+            if (lists) {
                 const float wbf = wave_maxf(lb);
                 const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + A.skin : 0.f;
                 if (l == 0) {
@@ -1285,7 +1317,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         }
         namb_total += (int)__popcll(__ballot(amb));
     }
-    }   // tiles of this wave
+    }   // the wave's tile
     if (l == 0) {
         s_wstat[w][NSS] = (double)namb_total;
         s_wstat[w][NSS + 1] = (double)pairs * 64.0;
@@ -1295,8 +1327,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
 #ifdef GICP_STAMPS
     S.acc[7] = (unsigned long long)pairs;   // slot 7: rows scanned (not cycles)
     if (A.stamps && l == 0) {
-        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 16 + c] = S.acc[c];
-        for (int c = 0; c < 8; ++c) A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 16 + 8 + c] = S.cnt[c];
+        unsigned long long* o = A.stamps + ((int64_t)blockIdx.x * kCorrWaves + w) * 20;
+        for (int c = 0; c < 8; ++c) o[c] = S.acc[c];
+        for (int c = 0; c < 8; ++c) o[8 + c] = S.cnt[c];
+        o[16] = S.rt0;                                   // 100 MHz realtime: wave start / end
+        o[17] = __builtin_amdgcn_s_memrealtime();
+        o[18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        o[19] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
     }
 #endif
     __syncthreads();
@@ -1310,12 +1347,21 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < kCorrWaves; ++u) s += s_wstat[u][t];
-        __hip_atomic_store(&A.partials[(int64_t)blockIdx.x * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&A.partials[(int64_t)unit * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (A.order && threadIdx.x == 0 && unit < 8 * q8) {   // cost class of this unit for the next pass
+        const unsigned long long dur = __builtin_amdgcn_s_memtime() - wg_t0 + 1;
+        const int lg2 = 63 - __clzll(dur);
+        const int half = (dur >> (lg2 > 0 ? lg2 - 1 : 0)) & 1;   // sqrt(2) steps
+        const int k = min(kOrderBuckets - 1, max(0, 2 * lg2 + half - 24));
+        const int x = unit / q8, par = (A.pass + 1) & 1;
+        const int pos = atomicAdd(&A.order_cnt[(par * 8 + x) * kOrderBuckets + k], 1);
+        A.order[((int64_t)(par * 8 + x) * kOrderBuckets + k) * q8 + pos] = unit;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ng = (int)((gridDim.x + kGroupWG - 1) / kGroupWG);
-    const int g = (int)(blockIdx.x / kGroupWG);
+    const int g = unit / kGroupWG;   // the reduction follows the unit, not the launch order
     if (threadIdx.x == 0) {
         const int gn = min(kGroupWG, (int)gridDim.x - g * kGroupWG);
         s_last = __hip_atomic_fetch_add(&A.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
@@ -1328,7 +1374,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     if (!s_last) return;
     // rows [b0, b1) of `src` ([row][NSX]) summed per statistic in row order: 3 threads per statistic,
     // each with its loads all in flight before the first add, combined in fixed order through LDS
-    __shared__ double s_red[3][NSX];
+    // reduction scratch aliases the waves' staging LDS (every wave is past its walk here)
+    static_assert(sizeof(double) * 4 * NSX <= sizeof(WaveLds) * kCorrWaves, "reduction scratch fits the staging LDS");
+    double (*s_red)[NSX] = reinterpret_cast<double (*)[NSX]>(&s_lds[0]);
+    double* s_sum = reinterpret_cast<double*>(&s_lds[0]) + 3 * NSX;
     auto sum_rows = [&](const double* src, int b0, int b1, double* dst_stat) {
         constexpr int PART = 22;                                  // rows per thread per chunk
         constexpr int NP = (64 * kCorrWaves) / NSX >= 3 ? 3 : 1;  // threads per statistic
@@ -1366,9 +1415,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
         }
         __syncthreads();
     };
-    __shared__ double s_sum[NSX];
     {
-        const int b0 = g * kGroupWG, b1 = min((int)gridDim.x, b0 + kGroupWG);
+        const int b0 = g * kGroupWG, b1 = min(nunits, b0 + kGroupWG);
         sum_rows(A.partials, b0, b1, s_sum);
         for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves)
             __hip_atomic_store(&A.gpart[(int64_t)g * NSX + t], s_sum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1388,6 +1436,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) k_corr(CorrArgs A) {
     if (!s_last) return;
     sum_rows(A.gpart, 0, ng, s_sum);
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
+    // every workgroup has read this pass's order: its counts become the next pass's append target
+    if (A.order)
+        for (int t = threadIdx.x; t < 8 * kOrderBuckets; t += 64 * kCorrWaves)
+            A.order_cnt[(A.pass & 1) * 8 * kOrderBuckets + t] = 0;
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1674,19 +1726,10 @@ hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
     return hipGetLastError();
 }
 
-// One resident generation of workgroups (occupancy x CUs), fewer if there are fewer tiles.
-int corr_grid(int q_tiles, int dim) {
-    static int cap[4] = {0, 0, 0, 0};
-    if (!cap[dim]) {
-        int dev = 0, ncu = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (dim == 2) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_corr<2>, 64 * kCorrWaves, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_corr<3>, 64 * kCorrWaves, 0);
-        cap[dim] = std::max(1, ncu) * std::max(1, per);
-    }
-    const int need = (q_tiles + kCorrWaves - 1) / kCorrWaves;
-    return kCorrLoop ? std::min(need, cap[dim]) : need;
+// Workgroups (units) of a k_corr launch: kCorrWaves source tiles each.
+int corr_grid(int q_tiles, int /*dim*/) {
+    if (q_tiles <= 0) return 0;
+    return (q_tiles + kCorrWaves - 1) / kCorrWaves;
 }
 
 hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
