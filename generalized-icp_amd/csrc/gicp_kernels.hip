@@ -40,27 +40,25 @@ __device__ __forceinline__ float marg(const Margin& m, float d2) {
     return fmaf(m.a * 1.0001f, __builtin_amdgcn_sqrtf(d2), fmaf(m.c, d2, m.b));
 }
 
-// wave-wide min, result uniform (SGPR); same DPP pattern as wave_maxf
+// Wave-wide min / max of floats that are >= 0 or a negative "none" marker, result uniform
+// (SGPR): signed-integer compares on the bit patterns (monotonic for such values, no NaN
+// canonicalisation), each step one v_{min,max}_i32 with a DPP source: row_shr 1/2/4/8,
+// row_bcast 15/31, then readlane 63.
+#define GICP_WAVE_REDUCE(OP, ID, x)                                                      \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x111, 0xf, 0xf, false));               \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x112, 0xf, 0xf, false));               \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x114, 0xf, 0xf, false));               \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x118, 0xf, 0xf, false));               \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x142, 0xa, 0xf, false));               \
+    x = OP(x, __builtin_amdgcn_update_dpp(ID, x, 0x143, 0xc, 0xf, false));
 __device__ __forceinline__ float wave_minf(float v) {
     int x = __float_as_int(v);
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false))));
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false))));
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false))));
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false))));
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false))));
-    x = __float_as_int(fminf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false))));
+    GICP_WAVE_REDUCE(min, 0x7fffffff, x)
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
-
-// wave-wide max, result uniform (SGPR): DPP row_shr 1/2/4/8, row_bcast 15/31, readlane 63
 __device__ __forceinline__ float wave_maxf(float v) {
     int x = __float_as_int(v);
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x111, 0xf, 0xf, false))));
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x112, 0xf, 0xf, false))));
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x114, 0xf, 0xf, false))));
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x118, 0xf, 0xf, false))));
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x142, 0xa, 0xf, false))));
-    x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x143, 0xc, 0xf, false))));
+    GICP_WAVE_REDUCE(max, (int)0x80000000, x)
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
 __device__ __forceinline__ double wave_mind(double v) {
