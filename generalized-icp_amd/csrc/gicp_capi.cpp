@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <thread>
 #include <new>
 #include <string>
 #include <vector>
@@ -234,11 +235,12 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
         for (int a = 0; a < dim; ++a)
             g[(size_t)i * dim + a] = (uint16_t)(dim == 3 ? compact3(c >> a) : compact2(c >> a));
     }
-    auto cut = [&](int E, bool emit) -> int64_t {
-        int64_t nt = 0, i0 = 0;
+    // greedy cut of points [b, e) (a forced break at b); appends (start, count) pairs if `out`
+    auto cut_seg = [&](int64_t b, int64_t e, int E, std::vector<int32_t>* out) -> int64_t {
+        int64_t nt = 0, i0 = b;
         int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-        for (int64_t i = 0; i <= n; ++i) {
-            bool brk = i == n || i - i0 == 64;
+        for (int64_t i = b; i <= e; ++i) {
+            bool brk = i == e || i - i0 == 64;
             if (!brk && i > i0) {
                 for (int a = 0; a < dim; ++a) {
                     const int v = g[(size_t)i * dim + a];
@@ -247,14 +249,13 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
             }
             if (brk && i > i0) {
                 ++nt;
-                if (emit) {
-                    start.push_back((int32_t)i0);
-                    count.push_back((int32_t)(i - i0));
-                    first_code.push_back(codes[i0]);
+                if (out) {
+                    out->push_back((int32_t)i0);
+                    out->push_back((int32_t)(i - i0));
                 }
                 i0 = i;
             }
-            if (i == n) break;
+            if (i == e) break;
             if (i == i0) {
                 for (int a = 0; a < dim; ++a) lo[a] = hi[a] = g[(size_t)i * dim + a];
             } else {
@@ -266,14 +267,44 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
         }
         return nt;
     };
-    const int emax = (1 << bits);
-    int E = emax;
-    for (double e = 2.0; e < emax; e *= 1.189207115) {   // 2^(1/4)
-        if (cut((int)e, false) <= target) {
-            E = (int)e;
-            break;
-        }
+    // 16 fixed segments (independent of the host's core count, so the tiling is deterministic),
+    // cut concurrently
+    constexpr int kSeg = 16;
+    std::vector<std::vector<int32_t>> seg_out(kSeg);
+    auto cut = [&](int E, bool emit) -> int64_t {
+        int64_t nt_seg[kSeg] = {};
+        auto work = [&](int s0, int s1) {
+            for (int k = s0; k < s1; ++k) {
+                if (emit) seg_out[k].clear();
+                nt_seg[k] = cut_seg(n * k / kSeg, n * (k + 1) / kSeg, E, emit ? &seg_out[k] : nullptr);
+            }
+        };
+        const int nth = (int)std::max(1u, std::min<unsigned>(kSeg, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(work, kSeg * t / nth, kSeg * (t + 1) / nth);
+        work(0, kSeg / nth);
+        for (auto& x : th) x.join();
+        int64_t nt = 0;
+        for (int k = 0; k < kSeg; ++k) nt += nt_seg[k];
+        if (emit)
+            for (int k = 0; k < kSeg; ++k)
+                for (size_t j = 0; j < seg_out[k].size(); j += 2) {
+                    start.push_back(seg_out[k][j]);
+                    count.push_back(seg_out[k][j + 1]);
+                    first_code.push_back(codes[seg_out[k][j]]);
+                }
+        return nt;
+    };
+    // smallest cap on the grid E_k = 2 * 2^(k/4) meeting the budget (the count falls as E grows):
+    // binary search over k
+    auto cap_of = [](int k) { return (int)(2.0 * std::pow(2.0, k / 4.0)); };
+    int klo = 0, khi = 4 * (bits - 1);   // cap_of(khi) = 2^bits: one Morton run per tile
+    while (klo < khi) {
+        const int km = (klo + khi) / 2;
+        if (cut(cap_of(km), false) <= target) khi = km;
+        else klo = km + 1;
     }
+    const int E = cap_of(klo);
     start.clear();
     count.clear();
     first_code.clear();
@@ -286,6 +317,18 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
                  int nshards, bool cov_all) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
+    const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
+    auto tprev = std::chrono::steady_clock::now();
+    std::string tlog;
+    auto tick = [&](const char* what) {
+        if (!verbose) return;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const auto t = std::chrono::steady_clock::now();
+        char b[64];
+        std::snprintf(b, sizeof b, " %s %.1f", what, std::chrono::duration<double, std::milli>(t - tprev).count());
+        tlog += b;
+        tprev = t;
+    };
     for (int64_t i = 0; i < n * dim; ++i)
         if (!std::isfinite(xyz[i])) throw Fail{GICP_E_INVALID, "cloud contains non-finite coordinates"};
     cl.release();
@@ -306,6 +349,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     ext = ext * (1.0 + 1e-9) + 1e-12 * (1.0 + std::fabs(mn[0]));
     for (int a = 0; a < 3; ++a) cl.lo[a] = a < dim ? mn[a] : 0.0;
     cl.scale = std::ldexp(1.0, cl.bits) / ext;
+    tick("host-scan");
 
     hipStream_t st = c->stream;
     double* d_in = nullptr;
@@ -328,12 +372,15 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         HIPCHK(hipMalloc(&d_tmp, tmp_bytes + 16));
         HIPCHK(rocprim::radix_sort_pairs(d_tmp, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
                                          st));
+        tick("upload+sort");
         std::vector<uint32_t> codes(n);
         HIPCHK(hipMemcpyAsync(codes.data(), d_codes_s, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        tick("codes-d2h");
         std::vector<int32_t> tstart, tcount;
         std::vector<uint32_t> tcode;
         build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level);
+        tick("tiling");
         cl.ntiles = (int)tstart.size();
         cl.nblocks = (cl.ntiles + kBlockTiles - 1) / kBlockTiles;
         std::vector<TileInfo> ti(cl.ntiles);
@@ -360,10 +407,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         HIPCHK(hipMemcpyAsync(&rho_bits, d_rho, sizeof(unsigned), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         std::memcpy(&cl.rho, &rho_bits, sizeof(float));
-        if (const char* e = std::getenv("GICP_VERBOSE"))
-            if (e[0] == '1')
-                std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f\n",
-                             (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho);
+        tick("tiles");
 
         // surface covariances (gicp.py:19-35) for this rank's query tiles
         int qb = 0, qe = cl.ntiles;
@@ -393,6 +437,10 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         cl.cov_ready = true;
         cl.cov_q_begin = qb;
         cl.cov_q_end = qe;
+        tick("covariances");
+        if (verbose)
+            std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f | ms:%s\n",
+                         (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho, tlog.c_str());
     } catch (...) {
         dfree(d_in);
         dfree(d_codes);
