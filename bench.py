@@ -51,6 +51,21 @@ def workload(n, dim):
         f"2d_segments_{n // 1000}k_k6"
 
 
+def measured_traffic(workload):
+    """HBM-side bytes per k_corr launch from the newest committed PMC summary of this workload
+    (scripts/profile_round.sh -> profiles/rNN/pmc_traffic.json); the counters cannot be read
+    in-process, so bench.py reports the profiled value of the same command and names its file."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(src, tgt, kw, workers, iters=1):
     """The oracle (NumPy/SciPy restatement) on the host: setup + `iters` outer iterations."""
     from scipy.spatial import cKDTree
@@ -130,6 +145,7 @@ def main():
     alg_bytes = BYTES_PER_POINT * (n_shard + a.n)
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
     pairs = res["pairs_evaluated"] / world
+    traffic, traffic_src = measured_traffic(name) if world == 1 else (None, None)
     line = {
         "metric": "GICP iterations/sec (and ms/iter) at N points, 1/2/4/8 GPU; final transform error",
         "value": a.steps / elapsed,
@@ -147,7 +163,7 @@ def main():
                    "k": 20 if a.dim == 3 else 6, **kw,
                    "parallelism": f"dp{world} (source shards; RCCL all-reduce of 74 fp64 per iteration)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_corr", "kernel_avg_ms": corr_avg_ms, "alg_bytes_per_launch": alg_bytes},
         "valu": {"pairs_per_launch": pairs, "tflops": pairs * FLOP_PER_PAIR / (corr_avg_ms * 1e-3) / 1e12,
                  "peak_tflops": FP32_PEAK_TFLOPS,

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round profile of the default bench command: kernel-trace stats, per-iteration trace, PMC
+# passes (instruction mix, waits) and the HBM-side traffic summary.  Output: gpurun_out/$1/.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-prof}
+mkdir -p $OUT
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o t --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/trace.err || { echo trace failed; exit 1; }
+python3 scripts/trace_iters.py $OUT/trace 30 > $OUT/iterations.txt
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAVE_CYCLES" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" \
+           "FETCH_SIZE GRBM_GUI_ACTIVE" \
+           "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set -d $OUT/pmc/p$i -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/pmc_p$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+done
+python3 scripts/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt
+python3 scripts/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json k_corr 3d_room_1000k_1000k_k20
+echo done
