@@ -152,6 +152,7 @@ struct gicp_ctx {
     int pass = 0;
     bool use_lists = true;
     bool use_order = true;            // GICP_NO_ORDER=1: identity workgroup order
+    double skin_frac = 0.2;           // candidate-list skin as a fraction of d_c (GICP_SKIN)
     double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -534,7 +535,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.poses = c->d_poses;
     a.pass = ++c->pass;
     a.use_lists = c->use_lists ? 1 : 0;
-    a.skin = (float)(0.2 * dc);
+    a.skin = (float)(c->skin_frac * dc);
+    a.gap_slack = (float)std::ldexp(std::sqrt((double)a.search2) + 2.0 * c->tgt.rho + 2.0 * c->src.rho, -19);
     return a;
 }
 
@@ -712,6 +714,7 @@ int gicp_create(gicp_ctx** out, int device) {
     c->device = device;
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_NO_ORDER")) c->use_order = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;

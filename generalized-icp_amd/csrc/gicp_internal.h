@@ -109,6 +109,7 @@ struct CorrArgs {
     double* gpart;            // [kMaxGroups][nstat_ext] group partials
     int32_t single_pass;      // 1: run even if state->converged (gicp_iterate)
     float search2;            // fp32 screen bound (d_c^2 + margins)
+    float gap_slack;          // rounding slack S of the box tests (search radius + 2 rho_t, x 2^-19)
     double dc;                // d_c, fp64, inclusive (distance > d_c rejects)
     Margin mg;
     int32_t* hint;            // [src.ntiles] best target tile of the previous pass

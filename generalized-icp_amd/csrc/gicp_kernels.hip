@@ -72,6 +72,8 @@ __device__ __forceinline__ double wave_maxd(double v) {
     return v;
 }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+// any lane: the ballot's scalar result tested directly (no bool -> int -> compare round trip)
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
 // Diagnostic-only phase timer (build with `make STAMPS=1`): s_memtime cycles per phase per wave.
 // 0 setup, 1 traversal tests, 2 tile need-test + staging, 3 row scan, 4 fp64 fallback,
@@ -503,6 +505,37 @@ __device__ __forceinline__ unsigned sub_mask(const TileInfo& ti, const float* pr
             g2 = fmaf(gg, gg, g2);
         }
         if (__any(valid && g2 <= bound)) m |= 1u << g;
+    }
+    return m;
+}
+
+// k_corr's forms of lane_gap2 / sub_mask: no per-axis rounding slack; the caller compares against a
+// bound inflated once by the launch-uniform slack S (CorrArgs::gap_slack: rounding of coordinates
+// of magnitude <= sqrt(search2) + 2 rho_t, the only ones whose test can matter)
+template <int D>
+__device__ __forceinline__ float lane_gap2_ns(const Query<D>& q, const TileInfo& ti, float* pr) {
+    float g2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        pr[a] = q.pw[a] + (float)(q.ow[a] - ti.c[a]);
+        const float g = fmaxf(fabsf(pr[a]) - ti.h[a], 0.f);
+        g2 = fmaf(g, g, g2);
+    }
+    return g2;
+}
+template <int D>
+__device__ __forceinline__ unsigned sub_mask_ns(const TileInfo& ti, const float* pr, bool valid, float bound) {
+    unsigned m = 0;
+#pragma unroll
+    for (int g = 0; g < kSub; ++g) {
+        if (16 * g >= ti.count) break;
+        float g2 = 0.f;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const float gg = fmaxf(fabsf(pr[a] - ti.sc[g][a]) - ti.sh[g][a], 0.f);
+            g2 = fmaf(gg, gg, g2);
+        }
+        if (wave_any(valid && g2 <= bound)) m |= 1u << g;
     }
     return m;
 }
@@ -960,18 +993,25 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
         };
         float lb = lane_bound();   // refreshed after every merge
+        // lb inflated by the rounding slack, for the slack-free box tests
+        auto inflate = [&](float w) -> float {
+            if (w < 0.f) return w;
+            const float r = __builtin_amdgcn_sqrtf(w) * 1.0001f + 2.f * A.gap_slack;
+            return r * r;
+        };
+        float lbx = inflate(lb);
         // visit target tile Tt; `pre` = its coordinates already loaded (prefetch) or null
         auto visit_pre = [&](int Tt, const float4* pre) -> bool {
             S.mark(1);
             S.count(0);
             const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
-            const bool need = lane_gap2<D>(q, ti, pr) <= lb;
-            if (!__any(need)) {
+            const bool need = lane_gap2_ns<D>(q, ti, pr) <= lbx;
+            if (!wave_any(need)) {
                 S.mark(2);
                 return false;
             }
-            const unsigned sub = sub_mask<D>(ti, pr, q.valid, lb);
+            const unsigned sub = sub_mask_ns<D>(ti, pr, q.valid, lbx);
             if (pre) stage_f32_from(*pre, L);
             else stage_f32(tg, ti, L);
             S.mark(2);
@@ -991,6 +1031,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 sec = min(sec, tb);
             }
             lb = lane_bound();
+            lbx = inflate(lb);
             wave_sync();
             S.mark(3);
             return true;
@@ -1074,6 +1115,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 best = sec = init;
                 best_tile = -1;
                 lb = lane_bound();
+                lbx = inflate(lb);
                 ++list_rebuilds;
             }
         }
