@@ -72,6 +72,24 @@ __device__ __forceinline__ double wave_maxd(double v) {
     return v;
 }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+// ascending bitonic sort of one (key, val) pair per lane across the wave; ties by val (deterministic)
+__device__ __forceinline__ void wave_sort64(float& key, int& val) {
+    const int l = __lane_id();
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const float pk = __shfl_xor(key, j);
+            const int pv = __shfl_xor(val, j);
+            const bool take_min = ((l & k) == 0) == ((l & j) == 0);
+            const bool less = pk < key || (pk == key && pv < val);
+            const bool greater = pk > key || (pk == key && pv > val);
+            if (take_min ? less : greater) {
+                key = pk;
+                val = pv;
+            }
+        }
+}
 // any lane: the ballot's scalar result tested directly (no bool -> int -> compare round trip)
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
@@ -1081,13 +1099,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             float wb = wave_maxf(lb);
             uint64_t rem = __ballot(l < nl && eg2 <= wb);
             // nearest remaining entry (wave-uniform lane index), -1 if none
-            auto pick = [&]() -> int {
-                if (!rem) return -1;
-                const bool in = (rem >> l) & 1ull;
-                const float m = wave_minf(in ? eg2 : 3e38f);
-                const uint64_t c = __ballot(in && eg2 == m);
-                return __ffsll((unsigned long long)c) - 1;
-            };
+            // lists are stored nearest-first (sorted when built): the next entry is the lowest set bit
+            auto pick = [&]() -> int { return rem ? __ffsll((unsigned long long)rem) - 1 : -1; };
             int k = pick();
             float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
             if (k >= 0) pv = load_rel(tg, __builtin_amdgcn_readlane(est, k), __builtin_amdgcn_readlane(ecnt, k));
@@ -1121,8 +1134,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         if (!use) {
             int ncol = 0;
+            int cent = 0x7fffffff;   // lane k: collected entry k
             auto collect = [&](int Tt) {
-                if (ncol < kListMax && l == 0) A.list[(int64_t)T * kListMax + ncol] = Tt;
+                if (l == ncol) cent = Tt;
                 ++ncol;
             };
             traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, lists ? A.skin : 0.f,
@@ -1130,6 +1144,19 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (lists) {
                 const float wbf = wave_maxf(lb);
                 const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + A.skin : 0.f;
+                if (ncol <= kListMax) {   // store nearest-first: by centre distance to the wave box
+                    float key = 3e38f;
+                    if (l < ncol) {
+                        key = 0.f;
+#pragma unroll
+                        for (int a = 0; a < D; ++a) {
+                            const float d = (float)(tg.tiles[cent].c[a] - q.ow[a]);
+                            key = fmaf(d, d, key);
+                        }
+                    }
+                    wave_sort64(key, cent);
+                    if (l < ncol) A.list[(int64_t)T * kListMax + l] = cent;
+                }
                 if (l == 0) {
                     A.list_len[T] = min(ncol, kListMax);
                     A.list_rcert[T] = r;
