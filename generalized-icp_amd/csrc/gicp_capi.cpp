@@ -547,7 +547,7 @@ void allreduce_stats(gicp_ctx* c) {
     if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
 }
 
-#ifdef GICP_STAMPS
+#if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
 // Diagnostic build: per wave 8 phase-cycle slots (7 = rows scanned) + 8 event counters.
 void print_stamps(const unsigned long long* d_stamps, size_t nst) {
     constexpr int W = 20;
@@ -630,7 +630,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     }
     const int nsx = nstat_ext(d);
     const int grid = corr_grid(c->q_end - c->q_begin, d);
-#ifdef GICP_STAMPS
+#if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
     static unsigned long long* d_stamps = nullptr;
     static size_t stamps_cap = 0;
     const size_t nst = (size_t)std::max(1, grid) * kCorrWaves * 20;
@@ -654,7 +654,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
             HIPCHK(hipMemcpyAsync(dbg->distance, c->d_dbg_dist, sizeof(double) * n, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
-#ifdef GICP_STAMPS
+#if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
     print_stamps(d_stamps, nst);
 #endif
     const int ns = nstat(d);

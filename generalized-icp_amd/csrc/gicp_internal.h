@@ -32,8 +32,8 @@ struct __attribute__((aligned(16))) TileInfo {
     int32_t start;    // first sorted point
     int32_t count;    // 1..64
     float radius;     // max |rel32| norm
-    float sc[kSub][3];  // sub-tile box centres (rows 16g..16g+15), relative to c, fp32
-    float sh[kSub][3];  // sub-tile box half-extents (cover every rel32 of the sub-tile)
+    float sc[3][kSub];  // sub-tile box centres (rows 16g..16g+15) relative to c, fp32, axis-major
+    float sh[3][kSub];  // sub-tile box half-extents (cover every rel32 of the sub-tile), axis-major
 };
 
 struct __attribute__((aligned(16))) BlockInfo {

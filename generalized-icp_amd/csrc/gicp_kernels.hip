@@ -113,6 +113,12 @@ struct Stamps {
     // 5 traversal block tests, 6 traversal candidate blocks, 7 fp64 fallback tiles
     unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     __device__ __forceinline__ void count(int k, unsigned v = 1) { cnt[k] += v; }
+#elif defined(GICP_TIMELINE)   // `make VARIANT=tl VDEFS=-DGICP_TIMELINE`: wave start/end only
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void count(int, unsigned = 1) {}
 #else
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
@@ -228,8 +234,8 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
             const float cc = empty ? 0.f : 0.5f * (smn[a] + smx[a]);
             // half-extent rounded up so the box covers both extremes exactly
             const float hh = empty ? -1e30f : fmaxf(smx[a] - cc, cc - smn[a]) * (1.0f + 2.4e-7f);
-            t.sc[g][a] = cc;
-            t.sh[g][a] = hh;
+            t.sc[a][g] = cc;
+            t.sh[a][g] = hh;
         }
     }
     if (l == 0) {
@@ -419,8 +425,8 @@ __device__ __forceinline__ TileInfo tile_meta(const DevCloud& db, int T) {
     for (int g = 0; g < kSub; ++g)
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            t.sc[g][a] = ct->sc[g][a];
-            t.sh[g][a] = ct->sh[g][a];
+            t.sc[a][g] = ct->sc[a][g];
+            t.sh[a][g] = ct->sh[a][g];
         }
     return t;
 }
@@ -517,8 +523,8 @@ __device__ __forceinline__ unsigned sub_mask(const TileInfo& ti, const float* pr
         float g2 = 0.f;
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            const float dl = fabsf(pr[a] - ti.sc[g][a]);
-            float gg = dl - ti.sh[g][a] - (dl + ti.sh[g][a] + fabsf(pr[a])) * 9.5367431640625e-7f;
+            const float dl = fabsf(pr[a] - ti.sc[a][g]);
+            float gg = dl - ti.sh[a][g] - (dl + ti.sh[a][g] + fabsf(pr[a])) * 9.5367431640625e-7f;
             gg = fmaxf(gg, 0.f);
             g2 = fmaf(gg, gg, g2);
         }
@@ -542,18 +548,24 @@ __device__ __forceinline__ float lane_gap2_ns(const Query<D>& q, const TileInfo&
     return g2;
 }
 template <int D>
-__device__ __forceinline__ unsigned sub_mask_ns(const TileInfo& ti, const float* pr, bool valid, float bound) {
+__device__ __forceinline__ unsigned sub_mask_ns(const TileInfo& ti, const float* pr, float bound /* < 0: lane off */) {
+    // two sub-boxes per packed op (sc/sh are axis-major, so boxes g and g+1 of an axis are adjacent):
+    // g = max(max(d, -d) - sh, 0), g2 += g * g
+    typedef float f2v __attribute__((ext_vector_type(2)));
     unsigned m = 0;
 #pragma unroll
-    for (int g = 0; g < kSub; ++g) {
+    for (int g = 0; g < kSub; g += 2) {
         if (16 * g >= ti.count) break;
-        float g2 = 0.f;
+        f2v g2 = {0.f, 0.f};
 #pragma unroll
         for (int a = 0; a < D; ++a) {
-            const float gg = fmaxf(fabsf(pr[a] - ti.sc[g][a]) - ti.sh[g][a], 0.f);
-            g2 = fmaf(gg, gg, g2);
+            const f2v d = f2v{pr[a], pr[a]} - f2v{ti.sc[a][g], ti.sc[a][g + 1]};
+            const f2v ad = __builtin_elementwise_max(d, -d);
+            const f2v gg = __builtin_elementwise_max(ad - f2v{ti.sh[a][g], ti.sh[a][g + 1]}, f2v{0.f, 0.f});
+            g2 = __builtin_elementwise_fma(gg, gg, g2);
         }
-        if (wave_any(valid && g2 <= bound)) m |= 1u << g;
+        if (wave_any(g2.x <= bound)) m |= 1u << g;
+        if (16 * (g + 1) < ti.count && wave_any(g2.y <= bound)) m |= 2u << g;
     }
     return m;
 }
@@ -855,7 +867,13 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 // <= 90 leaves 7 and <= 72 (with <= 64 VGPRs) 8 (scripts/probes/occupancy.hip measures it; the
 // compiler's own occupancy estimate does not model it).
 #ifndef GICP_CORR_ATTR
+#if defined(GICP_CORR_WAVES_PER_EU)
+#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(GICP_CORR_WAVES_PER_EU, GICP_CORR_WAVES_PER_EU)))
+#elif defined(GICP_TIMELINE)   // keep the diagnostic build at the product's 7 waves per SIMD
+#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(7, 7)))
+#else
 #define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR)))
+#endif
 #endif
 #ifndef GICP_CORR_SGPR
 #define GICP_CORR_SGPR 88
@@ -925,6 +943,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
     Stamps S;
     S.start();
+#ifdef GICP_TIMELINE
+    if (A.stamps && l == 0)   // stored at once: no register held across the wave
+        A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 20 + 16] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (A.use_lists && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
         double* ring = A.poses + (A.pass % kPoseRing) * 12;
         for (int a = 0; a < 3; ++a) {
@@ -1024,12 +1046,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             S.count(0);
             const TileInfo ti = tile_meta(tg, Tt);
             float pr[D];
-            const bool need = lane_gap2_ns<D>(q, ti, pr) <= lbx;
-            if (!wave_any(need)) {
+            // lbx < 0 on lanes without a query: one compare per test
+            if (!wave_any(lane_gap2_ns<D>(q, ti, pr) <= lbx)) {
                 S.mark(2);
                 return false;
             }
-            const unsigned sub = sub_mask_ns<D>(ti, pr, q.valid, lbx);
+            const unsigned sub = sub_mask_ns<D>(ti, pr, lbx);
             if (pre) stage_f32_from(*pre, L);
             else stage_f32(tg, ti, L);
             S.mark(2);
@@ -1391,13 +1413,19 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         s_wstat[w][NSS + 2] = (double)list_rebuilds;
     }
     S.mark(6);
-#ifdef GICP_STAMPS
-    S.acc[7] = (unsigned long long)pairs;   // slot 7: rows scanned (not cycles)
+#if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
+#ifndef GICP_TIMELINE
+    S.acc[7] = (unsigned long long)pairs;
+#endif   // slot 7: rows scanned (not cycles)
     if (A.stamps && l == 0) {
         unsigned long long* o = A.stamps + ((int64_t)blockIdx.x * kCorrWaves + w) * 20;
+#ifndef GICP_TIMELINE
         for (int c = 0; c < 8; ++c) o[c] = S.acc[c];
         for (int c = 0; c < 8; ++c) o[8 + c] = S.cnt[c];
+#endif
+#ifndef GICP_TIMELINE
         o[16] = S.rt0;                                   // 100 MHz realtime: wave start / end
+#endif
         o[17] = __builtin_amdgcn_s_memrealtime();
         o[18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
         o[19] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
