@@ -1,0 +1,93 @@
+"""C5 (BASELINE.json configs[4]): scan-to-scan odometry over a synthetic spinning-LiDAR stream
+(64 x 1563 rays ~ 100k points per frame) through the C2 room, one MI355X.
+
+    python bench_odometry.py [--frames 1000] [--max-iterations 30] [--fixed]
+
+Prints one JSON line: GICP iterations/sec over the registration loops, frames/sec end to end
+(upload + index + covariances + registration per frame), setup per frame, and the trajectory
+error against the generating poses.  Scans are generated before the timed stream (on the GPU
+through torch when available — data plumbing, not the measured path)."""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "generalized-icp_amd"))
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--beams", type=int, default=64)
+    ap.add_argument("--azimuths", type=int, default=1563)
+    ap.add_argument("--max-iterations", type=int, default=30)
+    ap.add_argument("--fixed", action="store_true", help="fixed iterations (convergence disabled)")
+    ap.add_argument("--tolerance", type=float, default=1e-6)
+    a = ap.parse_args()
+    from gicp import synthetic as S
+    from gicp.odometry import Odometry
+    xp, dev = None, None
+    try:
+        import torch
+        if torch.cuda.is_available():
+            xp, dev = torch, "cuda"
+    except ImportError:
+        pass
+    t0 = time.perf_counter()
+    frames = list(S.lidar_stream(a.frames, a.beams, a.azimuths, xp=xp, device=dev))
+    gen_s = time.perf_counter() - t0
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    import gicp
+    p = gicp.default_params(3, max_iterations=a.max_iterations, tolerance=a.tolerance,
+                            fixed_iterations=1 if a.fixed else 0, **kw)
+    odo = Odometry(3, params=p)
+    # warm-up on the first two frames (library init, allocation), then restart the stream
+    odo.step(frames[0][0])
+    odo.step(frames[1][0])
+    odo.reset()   # same device context and buffers, fresh stream
+    t1 = time.perf_counter()
+    errs = []
+    for k, (scan, pose) in enumerate(frames):
+        T, res = odo.step(scan)
+        if T is not None:
+            Ttrue = np.linalg.inv(pose) @ frames[k - 1][1]
+            errs.append((S.rotation_angle_error(T, Ttrue), S.translation_error(T, Ttrue)))
+    wall = time.perf_counter() - t1
+    P0 = frames[0][1]
+    est_end = P0 @ odo.pose
+    true_end = frames[-1][1]
+    errs = np.asarray(errs)
+    it = odo.timing["iterations"]
+    line = {
+        "metric": "GICP iterations/sec, scan-to-scan odometry stream (C5)",
+        "value": it / odo.timing["align_s"],
+        "unit": "it/s",
+        "n_gpus": 1,
+        "frames": a.frames,
+        "frames_per_s": (a.frames - 1) / wall,
+        "iterations_total": it,
+        "iterations_per_frame": it / max(1, a.frames - 1),
+        "setup_ms_per_frame": odo.timing["setup_s"] * 1e3 / a.frames,
+        "align_ms_per_frame": odo.timing["align_s"] * 1e3 / max(1, a.frames - 1),
+        "higher_is_better": True,
+        "dtype": "f32-screen+f64",
+        "data": f"synthetic spinning LiDAR, {a.beams}x{a.azimuths} rays, C2 room (generated in {gen_s:.1f} s, "
+                f"{'torch/' + dev if xp else 'numpy'})",
+        "config": {"workload": f"c5_lidar_{a.frames}f", "points_per_frame": int(np.mean([len(f[0]) for f in frames])),
+                   "max_iterations": a.max_iterations, "fixed_iterations": bool(a.fixed), **kw},
+        "frame_error": {"rot_rad_median": float(np.median(errs[:, 0])), "rot_rad_max": float(errs[:, 0].max()),
+                        "trans_median": float(np.median(errs[:, 1])), "trans_max": float(errs[:, 1].max())},
+        "drift": {"trans": float(np.linalg.norm(est_end[:3, 3] - true_end[:3, 3])),
+                  "rot_rad": S.rotation_angle_error(est_end, true_end),
+                  "path_length": float(sum(np.linalg.norm(frames[k][1][:3, 3] - frames[k - 1][1][:3, 3])
+                                           for k in range(1, len(frames))))},
+    }
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,15 @@ void dfree(T*& p) {
     if (p) (void)hipFree(p);
     p = nullptr;
 }
+// grow-only device buffer: reallocates (contents dropped) only when n exceeds the capacity, with
+// headroom, so a stream of similar-sized clouds allocates once
+template <class T>
+void dreserve(T*& p, size_t& cap, size_t n) {
+    if (n <= cap && p) return;
+    const size_t want = std::max<size_t>({n, (size_t)(cap * 1.125), 1});
+    dalloc(p, want);
+    cap = want;
+}
 
 // One indexed cloud on the device.
 struct Cloud {
@@ -86,6 +95,21 @@ struct Cloud {
     bool cov_ready = false;
     int cov_q_begin = 0, cov_q_end = 0;  // tiles whose covariances were computed
 
+    size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
+    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0;
+    void reserve_points(int64_t np) {
+        dreserve(xyz64, cap_xyz, (size_t)np * 4);
+        dreserve(rel32, cap_rel, (size_t)np);
+        dreserve(cov, cap_cov, (size_t)np);
+        dreserve(perm, cap_perm, (size_t)np);
+        dreserve(inv, cap_inv, (size_t)np);
+        dreserve(ncount, cap_cnt, (size_t)np);
+    }
+    void reserve_tiles(int nt, int nb) {
+        dreserve(tiles, cap_tiles, (size_t)nt);
+        dreserve(blocks, cap_blocks, (size_t)nb);
+        dreserve(tile_code, cap_tcode, (size_t)nt);
+    }
     void release() {
         dfree(xyz64);
         dfree(rel32);
@@ -96,6 +120,7 @@ struct Cloud {
         dfree(tiles);
         dfree(blocks);
         dfree(tile_code);
+        cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
         n = 0;
         cov_ready = false;
     }
@@ -147,6 +172,13 @@ struct gicp_ctx {
     int32_t* d_list_pass = nullptr;
     float* d_list_rcert = nullptr;
     double* d_poses = nullptr;
+    // cloud-build scratch and per-source-tile arrays, grow-only (a frame stream allocates once)
+    double* s_in = nullptr;
+    uint32_t *s_codes = nullptr, *s_codes2 = nullptr;
+    int32_t* s_idx = nullptr;
+    unsigned char* s_sort = nullptr;
+    size_t cap_in = 0, cap_codes = 0, cap_codes2 = 0, cap_idx = 0, cap_sort = 0;
+    size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0, cap_order = 0;
     int32_t* d_order = nullptr;       // longest-first unit order (CorrArgs::order)
     int32_t* d_order_cnt = nullptr;
     int pass = 0;
@@ -332,9 +364,9 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     };
     for (int64_t i = 0; i < n * dim; ++i)
         if (!std::isfinite(xyz[i])) throw Fail{GICP_E_INVALID, "cloud contains non-finite coordinates"};
-    cl.release();
+    cl.n = 0;   // buffers are kept (grow-only) and reused
+    cl.cov_ready = false;
     cl.dim = dim;
-    cl.n = n;
     cl.bits = dim == 3 ? 10 : 16;
     double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
     for (int a = 0; a < dim; ++a) {
@@ -353,26 +385,25 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     tick("host-scan");
 
     hipStream_t st = c->stream;
-    double* d_in = nullptr;
-    uint32_t *d_codes = nullptr, *d_codes_s = nullptr;
-    int32_t* d_idx = nullptr;
-    void* d_tmp = nullptr;
-    try {
-        dalloc(d_in, (size_t)n * dim);
+    {
+        cl.reserve_points(n);
+        dreserve(c->s_in, c->cap_in, (size_t)n * dim);
+        dreserve(c->s_codes, c->cap_codes, (size_t)n);
+        dreserve(c->s_codes2, c->cap_codes2, (size_t)n);
+        dreserve(c->s_idx, c->cap_idx, (size_t)n);
+        double* d_in = c->s_in;
+        uint32_t *d_codes = c->s_codes, *d_codes_s = c->s_codes2;
+        int32_t* d_idx = c->s_idx;
         HIPCHK(hipMemcpyAsync(d_in, xyz, sizeof(double) * n * dim, hipMemcpyHostToDevice, st));
-        dalloc(d_codes, n);
-        dalloc(d_codes_s, n);
-        dalloc(d_idx, n);
-        dalloc(cl.perm, n);
         DevCloud fr = cl.view();
         HIPCHK(launch_morton(d_in, n, dim, fr, d_codes, d_idx, st));
         size_t tmp_bytes = 0;
         const unsigned end_bit = (unsigned)(dim * cl.bits);
         HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
                                          st));
-        HIPCHK(hipMalloc(&d_tmp, tmp_bytes + 16));
-        HIPCHK(rocprim::radix_sort_pairs(d_tmp, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
-                                         st));
+        dreserve(c->s_sort, c->cap_sort, tmp_bytes + 16);
+        HIPCHK(rocprim::radix_sort_pairs((void*)c->s_sort, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0,
+                                         end_bit, st));
         tick("upload+sort");
         std::vector<uint32_t> codes(n);
         HIPCHK(hipMemcpyAsync(codes.data(), d_codes_s, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
@@ -390,14 +421,8 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
             ti[t].start = tstart[t];
             ti[t].count = tcount[t];
         }
-        dalloc(cl.tiles, cl.ntiles);
-        dalloc(cl.blocks, cl.nblocks);
-        dalloc(cl.tile_code, cl.ntiles);
-        dalloc(cl.xyz64, (size_t)n * 4);
-        dalloc(cl.rel32, n);
-        dalloc(cl.inv, n);
-        dalloc(cl.cov, n);
-        dalloc(cl.ncount, n);
+        cl.reserve_tiles(cl.ntiles, cl.nblocks);
+        cl.n = n;
         unsigned* d_rho = reinterpret_cast<unsigned*>(d_codes);  // reuse scratch
         HIPCHK(hipMemsetAsync(d_rho, 0, sizeof(unsigned), st));
         HIPCHK(hipMemcpyAsync(cl.tiles, ti.data(), sizeof(TileInfo) * cl.ntiles, hipMemcpyHostToDevice, st));
@@ -442,19 +467,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         if (verbose)
             std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f | ms:%s\n",
                          (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho, tlog.c_str());
-    } catch (...) {
-        dfree(d_in);
-        dfree(d_codes);
-        dfree(d_codes_s);
-        dfree(d_idx);
-        if (d_tmp) (void)hipFree(d_tmp);
-        throw;
     }
-    dfree(d_in);
-    dfree(d_codes);
-    dfree(d_codes_s);
-    dfree(d_idx);
-    (void)hipFree(d_tmp);
 }
 
 // Per-source-tile state that refers to target tiles (hints, candidate lists, heavy schedule):
@@ -476,14 +489,14 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     c->q_begin = (int)((int64_t)c->src.ntiles * shard / nshards);
     c->q_end = (int)((int64_t)c->src.ntiles * (shard + 1) / nshards);
     const int nt = std::max(1, c->src.ntiles);
-    dalloc(c->d_hint, nt);
-    dalloc(c->d_list, (size_t)nt * kListMax);
-    dalloc(c->d_list_len, nt);
-    dalloc(c->d_list_pass, nt);
-    dalloc(c->d_list_rcert, nt);
+    dreserve(c->d_hint, c->cap_hint, nt);
+    dreserve(c->d_list, c->cap_list, (size_t)nt * kListMax);
+    dreserve(c->d_list_len, c->cap_llen, nt);
+    dreserve(c->d_list_pass, c->cap_lpass, nt);
+    dreserve(c->d_list_rcert, c->cap_lrc, nt);
     if (!c->d_poses) dalloc(c->d_poses, (size_t)kPoseRing * 12);
     const int q8 = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim) / 8);
-    dalloc(c->d_order, (size_t)2 * 8 * kOrderBuckets * q8);
+    dreserve(c->d_order, c->cap_order, (size_t)2 * 8 * kOrderBuckets * q8);
     if (!c->d_order_cnt) dalloc(c->d_order_cnt, 2 * 8 * kOrderBuckets);
     reset_tile_state(c);
 }
@@ -761,6 +774,11 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_poses);
     dfree(c->d_order);
     dfree(c->d_order_cnt);
+    dfree(c->s_in);
+    dfree(c->s_codes);
+    dfree(c->s_codes2);
+    dfree(c->s_idx);
+    dfree(c->s_sort);
     if (c->h_state) (void)hipHostFree(c->h_state);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -821,9 +839,9 @@ int gicp_target_to_source(gicp_ctx* c, int shard, int nshards) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_target_to_source", [&] {
         if (!c->tgt.n) throw Fail{GICP_E_STATE, "no target to promote"};
-        c->src.release();
-        c->src = c->tgt;
-        c->tgt = Cloud();  // ownership moved
+        std::swap(c->src, c->tgt);   // the old source's buffers are kept for the next target
+        c->tgt.n = 0;
+        c->tgt.cov_ready = false;
         c->psrc = c->ptgt;
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));

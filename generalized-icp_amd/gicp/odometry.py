@@ -1,0 +1,85 @@
+"""Scan-to-scan odometry over a frame stream — the pattern of robot-visualization.py:239-265
+(SURVEY.md §8(f) rank 1, config C5), on the device.
+
+Each new scan becomes the target; the previous target, with its index and covariances already on
+the GPU, becomes the source (`gicp_target_to_source`, robot-visualization.py:250) — so per frame
+only the new scan is uploaded, sorted, tiled and given covariances.  `gicp(prev, cur)` maps the
+previous sensor frame into the current one (p_cur = T p_prev), so the sensor pose advances by
+T^-1: `composition='se3'` (default) is that exact SE(d) update; `composition='reference'` is the
+demo's first-order update (robot-visualization.py:257-265: translation -T[:2, d], yaw
+-atan2(T[1,0], T[0,0]), rotated by the last yaw), kept for trajectory comparisons with the demo.
+"""
+import math
+import time
+
+import numpy as np
+
+from . import Engine, default_params
+
+
+class Odometry:
+    def __init__(self, dim=3, params=None, device=0, composition="se3", init="constant_velocity", **kw):
+        if composition not in ("se3", "reference"):
+            raise ValueError("composition must be 'se3' or 'reference'")
+        if init not in ("identity", "constant_velocity"):
+            raise ValueError("init must be 'identity' or 'constant_velocity'")
+        self.dim = dim
+        self.params = params if params is not None else default_params(dim, **kw)
+        self.eng = Engine(device)
+        self.composition = composition
+        self.init = init
+        self.reset()
+
+    def reset(self):
+        """Start a new stream (the device context and its buffers are kept)."""
+        dim = self.dim
+        self.pose = np.eye(dim + 1)          # current sensor -> world (first frame = origin)
+        self.poses = [self.pose.copy()]
+        self.yaw_xy = (0.0, 0.0, 0.0)        # reference-formula state (x, y, yaw)
+        self.last_T = None
+        self.frames = 0
+        self.timing = {"setup_s": 0.0, "align_s": 0.0, "iterations": 0}
+
+    def step(self, scan):
+        """Add one scan; returns (T, result) of its registration against the previous scan, or
+        (None, None) for the first frame."""
+        scan = np.ascontiguousarray(np.asarray(scan, dtype=np.float64)[:, :self.dim])
+        t0 = time.perf_counter()
+        if self.frames > 0:
+            self.eng.target_to_source()
+        self.eng.set_target(scan, self.params)
+        t1 = time.perf_counter()
+        self.timing["setup_s"] += t1 - t0
+        self.frames += 1
+        if self.frames == 1:
+            return None, None
+        T0 = self.last_T if (self.init == "constant_velocity" and self.last_T is not None) else None
+        T, res = self.eng.align(T0, self.params)
+        self.timing["align_s"] += time.perf_counter() - t1
+        self.timing["iterations"] += res["iterations"]
+        self.last_T = T
+        self._integrate(T)
+        return T, res
+
+    def _integrate(self, T):
+        self.pose, self.yaw_xy = compose(self.pose, T, self.composition, self.yaw_xy)
+        self.poses.append(self.pose.copy())
+
+
+def compose(pose, T, composition="se3", yaw_xy=(0.0, 0.0, 0.0)):
+    """Advance the sensor pose by one registration T (p_cur = T p_prev).  Returns (pose, yaw_xy).
+    'se3': pose @ T^-1.  'reference': robot-visualization.py:257-265 — translation (-T[0,d], -T[1,d])
+    rotated by the last yaw, yaw += -atan2(T[1,0], T[0,0]) — rebuilt as a planar pose."""
+    d = T.shape[0] - 1
+    if composition == "se3":
+        return pose @ np.linalg.inv(T), tuple(yaw_xy)
+    x, y, yaw = yaw_xy
+    dx, dy = -T[0, d], -T[1, d]
+    dyaw = -math.atan2(T[1, 0], T[0, 0])
+    x, y = x + dx * math.cos(yaw) - dy * math.sin(yaw), y + dx * math.sin(yaw) + dy * math.cos(yaw)
+    yaw += dyaw
+    P = np.eye(d + 1)
+    c, s = math.cos(yaw), math.sin(yaw)
+    P[0, 0], P[0, 1], P[1, 0], P[1, 1] = c, -s, s, c
+    P[0, d], P[1, d] = x, y
+    return P, (x, y, yaw)

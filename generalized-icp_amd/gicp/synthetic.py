@@ -302,3 +302,119 @@ def rotation_angle_error(Ta, Tb):
 def translation_error(Ta, Tb):
     d = Ta.shape[0] - 1
     return float(np.linalg.norm(Ta[:d, d] - Tb[:d, d]))
+
+
+# ----------------------------------------------------------------------------- C5: LiDAR stream
+# a spinning LiDAR (64 beams, elevation -25..+15 deg, 1563 azimuths ~ 100k rays,
+# 100 m range, uniform +-0.02 m range noise mirroring robot-visualization.py:74) moving through the
+# C2 room; each frame is registered against the previous one (robot-visualization.py:239-265).
+
+def lidar_scene(radius=14.0, clearance=2.5, seed=42):
+    """The C2 room without the obstacles that block the circular sensor path (centre 0, `radius`)."""
+    sc = room_scene(seed=seed)
+    keep = []
+    for k in range(6, len(sc.rects), 6):     # boxes are 6 faces each after the 6 room rectangles
+        c = (sc.rects[k:k + 6, 0] + 0.5 * (sc.rects[k:k + 6, 1] + sc.rects[k:k + 6, 2])).mean(axis=0)
+        if abs(math.hypot(c[0], c[1]) - radius) > clearance + 1.5:
+            keep.extend(range(k, k + 6))
+    rects = np.concatenate([sc.rects[:6], sc.rects[keep]]) if keep else sc.rects[:6]
+    sph = [s for s in sc.spheres if abs(math.hypot(s[0], s[1]) - radius) > clearance + s[3]]
+    return Scene3D(rects, np.asarray(sph).reshape(-1, 4))
+
+
+def lidar_trajectory(frames, seed=7, radius=14.0, step=0.15, yaw_step_deg=0.5, height=1.8):
+    """Sensor-to-world poses (4x4) along a circle of `radius`: per frame ~`step` m and ~`yaw_step_deg`
+    of yaw (jittered by rng(seed)), the sensor looking along the path."""
+    rng = np.random.default_rng(seed)
+    poses = []
+    ang = 0.0
+    for _ in range(frames):
+        T = np.eye(4)
+        T[:3, :3] = axis_angle((0, 0, 1), ang + math.pi / 2)
+        T[:3, 3] = (radius * math.cos(ang), radius * math.sin(ang), height)
+        poses.append(T)
+        ang += step / radius * (1.0 + 0.2 * (rng.random() - 0.5))
+    return np.asarray(poses)
+
+
+def lidar_dirs(beams=64, azimuths=1563, elev=(-25.0, 15.0)):
+    el = np.radians(np.linspace(elev[0], elev[1], beams))
+    az = np.radians(np.arange(azimuths) * 360.0 / azimuths)
+    ce, se = np.cos(el)[:, None], np.sin(el)[:, None]
+    d = np.stack([ce * np.cos(az)[None, :], ce * np.sin(az)[None, :], np.broadcast_to(se, (beams, azimuths))], -1)
+    return d.reshape(-1, 3)
+
+
+def lidar_scan(scene, pose, dirs, rng, max_range=100.0, noise=0.02, xp=None, device=None):
+    """Points (sensor frame) where the rays `dirs` (sensor frame) from `pose` first hit `scene`.
+    `xp`: None for NumPy, or the `torch` module (then computed on `device`, returned as NumPy)."""
+    if xp is None:
+        return _lidar_scan_np(scene, pose, dirs, rng, max_range, noise)
+    return _lidar_scan_torch(xp, scene, pose, dirs, rng, max_range, noise, device)
+
+
+def _lidar_scan_np(scene, pose, dirs, rng, max_range, noise):
+    R, o = pose[:3, :3], pose[:3, 3]
+    D = dirs @ R.T                                            # world directions
+    best = np.full(len(D), np.inf)
+    for p0, e1, e2 in scene.rects:
+        n = np.cross(e1, e2)
+        dn = D @ n
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = ((p0 - o) @ n) / dn
+        h = o + t[:, None] * D - p0
+        a = (h @ e1) / (e1 @ e1)
+        b = (h @ e2) / (e2 @ e2)
+        ok = (t > 1e-6) & (a >= 0) & (a <= 1) & (b >= 0) & (b <= 1)
+        best = np.where(ok & (t < best), t, best)
+    for cx, cy, cz, r in scene.spheres:
+        oc = o - np.array([cx, cy, cz])
+        bq = D @ oc
+        disc = bq * bq - (oc @ oc - r * r)
+        sq = np.sqrt(np.maximum(disc, 0))
+        for t in (-bq - sq, -bq + sq):
+            ok = (disc >= 0) & (t > 1e-6) & (t < best)
+            best = np.where(ok, t, best)
+    hit = best < max_range
+    rng_ = best[hit] + rng.uniform(-noise, noise, hit.sum())
+    return dirs[hit] * rng_[:, None]
+
+
+def _lidar_scan_torch(torch, scene, pose, dirs, rng, max_range, noise, device):
+    f = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=device)
+    R, o = f(pose[:3, :3]), f(pose[:3, 3])
+    dt = f(dirs)
+    D = dt @ R.T
+    rects = f(scene.rects)
+    p0, e1, e2 = rects[:, 0], rects[:, 1], rects[:, 2]
+    n = torch.linalg.cross(e1, e2)
+    dn = D @ n.T                                              # rays x rects
+    t = ((p0 - o) * n).sum(1)[None, :] / dn
+    hx = o[None, None, :] + t[..., None] * D[:, None, :] - p0[None]
+    a = (hx * e1[None]).sum(-1) / (e1 * e1).sum(1)[None]
+    b = (hx * e2[None]).sum(-1) / (e2 * e2).sum(1)[None]
+    ok = (t > 1e-6) & (a >= 0) & (a <= 1) & (b >= 0) & (b <= 1)
+    best = torch.where(ok, t, torch.full_like(t, float("inf"))).min(1).values
+    if len(scene.spheres):
+        sp = f(scene.spheres)
+        oc = o[None, :] - sp[:, :3]                            # spheres x 3
+        bq = D @ oc.T                                          # rays x spheres
+        disc = bq * bq - ((oc * oc).sum(1) - sp[:, 3] ** 2)[None]
+        sq = torch.sqrt(torch.clamp(disc, min=0))
+        for tt in (-bq - sq, -bq + sq):
+            ok = (disc >= 0) & (tt > 1e-6)
+            best = torch.minimum(best, torch.where(ok, tt, torch.full_like(tt, float("inf"))).min(1).values)
+    best = best.cpu().numpy()
+    hit = best < max_range
+    rng_ = best[hit] + rng.uniform(-noise, noise, hit.sum())
+    return dirs[hit] * rng_[:, None]
+
+
+def lidar_stream(frames, beams=64, azimuths=1563, seed=7, xp=None, device=None):
+    """Generator of (scan_k, pose_k) for k = 0..frames-1 (scans in sensor coordinates)."""
+    scene = lidar_scene()
+    poses = lidar_trajectory(frames, seed=seed)
+    dirs = lidar_dirs(beams, azimuths)
+    rng = np.random.default_rng(seed + 1)
+    for k in range(frames):
+        yield lidar_scan(scene, poses[k], dirs, rng, xp=xp, device=device), poses[k]

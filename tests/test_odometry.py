@@ -1,0 +1,85 @@
+"""C5 odometry stream: pose composition on the CPU, the device stream
+against the oracle and the generating poses on the GPU."""
+import math
+
+import numpy as np
+import pytest
+
+from gicp import synthetic as S
+from gicp.odometry import compose
+
+
+def _planar(x, y, yaw, d=2):
+    P = np.eye(d + 1)
+    P[0, 0], P[0, 1], P[1, 0], P[1, 1] = math.cos(yaw), -math.sin(yaw), math.sin(yaw), math.cos(yaw)
+    P[0, d], P[1, d] = x, y
+    return P
+
+
+def test_compose_se3_recovers_trajectory():
+    poses = S.lidar_trajectory(20)
+    pose = poses[0].copy()
+    for k in range(1, 20):
+        T = np.linalg.inv(poses[k]) @ poses[k - 1]          # p_cur = T p_prev
+        pose, _ = compose(pose, T, "se3")
+        np.testing.assert_allclose(pose, poses[k], atol=1e-9)
+
+
+def test_compose_reference_formula():
+    """robot-visualization.py:257-265 literally: delta = -T[:2, 2], dyaw = -atan2(T10, T00), the
+    delta rotated by the previous yaw."""
+    rng = np.random.default_rng(3)
+    state = (0.0, 0.0, 0.0)
+    x, y, yaw = state
+    for _ in range(10):
+        T = _planar(*rng.normal(0, [2.0, 2.0, 0.05]))
+        P, state = compose(np.eye(3), T, "reference", state)
+        dx, dy, dyaw = -T[0, 2], -T[1, 2], -math.atan2(T[1, 0], T[0, 0])
+        x, y, yaw = x + dx * math.cos(yaw) - dy * math.sin(yaw), y + dx * math.sin(yaw) + dy * math.cos(yaw), yaw + dyaw
+        np.testing.assert_allclose(state, (x, y, yaw), atol=1e-12)
+        np.testing.assert_allclose(P, _planar(x, y, yaw), atol=1e-12)
+
+
+def test_lidar_scan_hits_and_noise():
+    scene = S.lidar_scene()
+    pose = S.lidar_trajectory(1)[0]
+    dirs = S.lidar_dirs(8, 90)
+    pts = S.lidar_scan(scene, pose, dirs, np.random.default_rng(0), noise=0.0)
+    assert len(pts) == len(dirs)                           # closed room: every ray hits
+    # noiseless hits lie on the scene: the world point is on some rectangle plane or sphere
+    w = pts @ pose[:3, :3].T + pose[:3, 3]
+    d_best = np.full(len(w), np.inf)
+    for p0, e1, e2 in scene.rects:
+        n = np.cross(e1, e2)
+        n /= np.linalg.norm(n)
+        d_best = np.minimum(d_best, np.abs((w - p0) @ n))
+    for cx, cy, cz, r in scene.spheres:
+        d_best = np.minimum(d_best, np.abs(np.linalg.norm(w - [cx, cy, cz], axis=1) - r))
+    assert np.max(d_best) < 1e-9
+
+
+@pytest.mark.gpu
+def test_odometry_stream_vs_oracle_and_truth():
+    from oracle import gicp_oracle as O
+    from gicp.odometry import Odometry
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    frames = list(S.lidar_stream(4, beams=16, azimuths=600))
+    import gicp
+    odo = Odometry(3, params=gicp.default_params(3, max_iterations=40, tolerance=1e-10, **kw), init="identity")
+    pose_oracle = np.eye(4)
+    for k, (scan, pose) in enumerate(frames):
+        T, res = odo.step(scan)
+        if T is None:
+            continue
+        prev = frames[k - 1][0]
+        To, *_ = O.gicp(prev, scan, max_iterations=40, tolerance=1e-10, **kw)
+        from golden_util import pose_err
+        a, t = pose_err(T, To)
+        assert a < 1e-6 and t < 1e-5, (k, a, t)              # same engine semantics as the oracle
+        pose_oracle = pose_oracle @ np.linalg.inv(To)
+        # against the generating motion (0.15 m, 0.6 deg): the reference's covariance model (in-plane
+        # to normal variance 10:1) under-registers the sliding direction of ring-pattern
+        # scans; both engines agree on that (above), so this is a sanity bound only
+        Ttrue = np.linalg.inv(pose) @ frames[k - 1][1]
+        assert S.rotation_angle_error(T, Ttrue) < 2e-3 and S.translation_error(T, Ttrue) < 0.1
+    np.testing.assert_allclose(odo.pose, pose_oracle, atol=1e-5)
