@@ -79,7 +79,7 @@ void dreserve(T*& p, size_t& cap, size_t n) {
 struct Cloud {
     int dim = 0;
     int64_t n = 0;
-    int ntiles = 0, nblocks = 0, level = 0, bits = 0;   // level: tile extent cap (grid cells)
+    int ntiles = 0, nblocks = 0, level = 0, bits = 0;   // level: tile extent-cap step k (cap 2^(1 + k/4) cells)
     double lo[3] = {0, 0, 0};
     double scale = 1.0;
     float rho = 0.f;
@@ -179,6 +179,7 @@ struct gicp_ctx {
     unsigned char* s_sort = nullptr;
     size_t cap_in = 0, cap_codes = 0, cap_codes2 = 0, cap_idx = 0, cap_sort = 0;
     size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0, cap_order = 0;
+    int cap_k_hint[4] = {0, 0, 0, 0};  // last tile extent-cap step per dimension (tiling warm start)
     int32_t* d_order = nullptr;       // longest-first unit order (CorrArgs::order)
     int32_t* d_order_cnt = nullptr;
     int pass = 0;
@@ -242,7 +243,7 @@ float screen_bound(const Margin& m, double d) {
 // tile count stays <= 1.35x the minimum ceil(n/64): tiles are as compact as that budget allows, and
 // the cap bounds the largest tile, which sets both the widest query wave and the loosest box.
 void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
-                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out) {
+                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out, int k_hint) {
     const int64_t n = (int64_t)codes.size();
     const int64_t target = (int64_t)(1.35 * std::ceil(n / 64.0)) + 2;
     // decode the grid coordinates once
@@ -271,16 +272,18 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
     // greedy cut of points [b, e) (a forced break at b); appends (start, count) pairs if `out`
     auto cut_seg = [&](int64_t b, int64_t e, int E, std::vector<int32_t>* out) -> int64_t {
         int64_t nt = 0, i0 = b;
-        int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-        for (int64_t i = b; i <= e; ++i) {
-            bool brk = i == e || i - i0 == 64;
-            if (!brk && i > i0) {
-                for (int a = 0; a < dim; ++a) {
-                    const int v = g[(size_t)i * dim + a];
-                    if (std::max(hi[a], v) - std::min(lo[a], v) > E) brk = true;
+        int lo0 = 0, lo1 = 0, lo2 = 0, hi0 = 0, hi1 = 0, hi2 = 0;
+        const uint16_t* gp = g.data();
+        for (int64_t i = b; i < e; ++i) {
+            const int v0 = gp[i * dim], v1 = gp[i * dim + 1], v2 = dim == 3 ? gp[i * dim + 2] : 0;
+            if (i > i0) {
+                const int n0 = std::min(lo0, v0), x0 = std::max(hi0, v0);
+                const int n1 = std::min(lo1, v1), x1 = std::max(hi1, v1);
+                const int n2 = std::min(lo2, v2), x2 = std::max(hi2, v2);
+                if (i - i0 < 64 && x0 - n0 <= E && x1 - n1 <= E && x2 - n2 <= E) {
+                    lo0 = n0, hi0 = x0, lo1 = n1, hi1 = x1, lo2 = n2, hi2 = x2;
+                    continue;
                 }
-            }
-            if (brk && i > i0) {
                 ++nt;
                 if (out) {
                     out->push_back((int32_t)i0);
@@ -288,14 +291,13 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
                 }
                 i0 = i;
             }
-            if (i == e) break;
-            if (i == i0) {
-                for (int a = 0; a < dim; ++a) lo[a] = hi[a] = g[(size_t)i * dim + a];
-            } else {
-                for (int a = 0; a < dim; ++a) {
-                    lo[a] = std::min(lo[a], (int)g[(size_t)i * dim + a]);
-                    hi[a] = std::max(hi[a], (int)g[(size_t)i * dim + a]);
-                }
+            lo0 = hi0 = v0, lo1 = hi1 = v1, lo2 = hi2 = v2;
+        }
+        if (e > i0) {
+            ++nt;
+            if (out) {
+                out->push_back((int32_t)i0);
+                out->push_back((int32_t)(e - i0));
             }
         }
         return nt;
@@ -312,7 +314,8 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
                 nt_seg[k] = cut_seg(n * k / kSeg, n * (k + 1) / kSeg, E, emit ? &seg_out[k] : nullptr);
             }
         };
-        const int nth = (int)std::max(1u, std::min<unsigned>(kSeg, std::thread::hardware_concurrency()));
+        // threads only pay off past a few hundred thousand points (spawn cost ~ tens of us each)
+        const int nth = n < 400000 ? 1 : (int)std::max(1u, std::min<unsigned>(kSeg, std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
         for (int t = 1; t < nth; ++t) th.emplace_back(work, kSeg * t / nth, kSeg * (t + 1) / nth);
         work(0, kSeg / nth);
@@ -329,20 +332,36 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
         return nt;
     };
     // smallest cap on the grid E_k = 2 * 2^(k/4) meeting the budget (the count falls as E grows):
+    // a short walk from the previous cloud's k when given (a frame stream changes little), else a
     // binary search over k
     auto cap_of = [](int k) { return (int)(2.0 * std::pow(2.0, k / 4.0)); };
-    int klo = 0, khi = 4 * (bits - 1);   // cap_of(khi) = 2^bits: one Morton run per tile
+    const int kmax = 4 * (bits - 1);   // cap_of(kmax) = 2^bits: one Morton run per tile
+    int klo = 0, khi = kmax;
+    if (k_hint > 0 && k_hint < kmax) {   // walk from the hint: usually hint feasible, hint-1 not
+        if (cut(cap_of(k_hint), false) <= target) {
+            khi = k_hint;
+            klo = k_hint - 1;
+            if (cut(cap_of(klo), false) <= target) {
+                khi = klo;
+                klo = 0;
+            } else {
+                klo = k_hint;
+            }
+        } else {
+            klo = k_hint + 1;
+        }
+    }
     while (klo < khi) {
         const int km = (klo + khi) / 2;
         if (cut(cap_of(km), false) <= target) khi = km;
         else klo = km + 1;
     }
     const int E = cap_of(klo);
+    cap_out = klo;
     start.clear();
     count.clear();
     first_code.clear();
     cut(E, true);
-    cap_out = E;
 }
 
 // Build the device index of a cloud and its per-point covariances for tiles [qb, qe) (qe < 0: all).
@@ -411,7 +430,8 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         tick("codes-d2h");
         std::vector<int32_t> tstart, tcount;
         std::vector<uint32_t> tcode;
-        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level);
+        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, c->cap_k_hint[dim & 3]);
+        c->cap_k_hint[dim & 3] = cl.level;
         tick("tiling");
         cl.ntiles = (int)tstart.size();
         cl.nblocks = (cl.ntiles + kBlockTiles - 1) / kBlockTiles;
