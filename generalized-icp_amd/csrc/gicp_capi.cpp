@@ -32,6 +32,8 @@ hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipSt
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t);
+hipError_t launch_top_weights(const double*, const int64_t*, int64_t, int, double*, int32_t*, int, double*, int64_t*,
+                              int64_t*, hipStream_t);
 int corr_grid(int, int);
 int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
 }  // namespace gicp
@@ -165,7 +167,12 @@ struct gicp_ctx {
     int64_t* d_dbg_idx = nullptr;
     double* d_dbg_w = nullptr;
     double* d_dbg_dist = nullptr;
+    double* d_dbg_det = nullptr;      // det(W) per source point (gicp_top_weights)
     size_t dbg_cap = 0;
+    bool top_ready = false;           // the last pass recorded det(W)
+    double* d_top_v = nullptr;        // top-k scratch: stage-1 candidates and outputs
+    int32_t* d_top_i = nullptr;
+    int64_t* d_top_out = nullptr;
     // per-source-tile candidate lists
     int32_t* d_list = nullptr;
     int32_t* d_list_len = nullptr;
@@ -192,7 +199,7 @@ struct gicp_ctx {
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
     // diagnostics of the last pass
-    double last_amb = 0.0, last_pairs = 0.0;
+    double last_amb = 0.0, last_pairs = 0.0, last_sq = 0.0;
     float last_corr_ms = 0.f, last_reduce_ms = 0.f;
     bool timing = false;
 };
@@ -220,6 +227,9 @@ gicp_params resolve(int dim, const gicp_params* in) {
     if (p.k_neighbors <= 0) p.k_neighbors = dim == 2 ? 6 : 20;
     if (p.min_neighbors <= 0) p.min_neighbors = dim;
     if (p.epsilon == 0.0) p.epsilon = 100.0;
+    if (p.cov_model < GICP_COV_PLANE_TO_PLANE || p.cov_model > GICP_COV_POINT_TO_PLANE)
+        throw Fail{GICP_E_INVALID, "cov_model must be GICP_COV_PLANE_TO_PLANE, _POINT_TO_POINT or _POINT_TO_PLANE"};
+    if (p.rotation_epsilon <= 0.0 && p.transformation_epsilon > 0.0) p.rotation_epsilon = 1.0 - p.transformation_epsilon;
     return p;
 }
 
@@ -570,6 +580,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.use_lists = c->use_lists ? 1 : 0;
     a.skin = (float)(c->skin_frac * dc);
     a.gap_slack = (float)std::ldexp(std::sqrt((double)a.search2) + 2.0 * c->tgt.rho + 2.0 * c->src.rho, -19);
+    a.cov_model = c->psrc.cov_model;
+    a.pl_inv = 1.0 / (c->ptgt.epsilon * (1.0 - c->ptgt.ratio));   // target m = sqrt(eps (1 - ratio)) n
     return a;
 }
 
@@ -649,17 +661,23 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     hs.converged_at = -1;
     HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
     CorrArgs a = corr_args(c, 1);
-    if (dbg && (dbg->index || dbg->weight || dbg->distance)) {
+    c->top_ready = false;
+    if (dbg && (dbg->index || dbg->weight || dbg->distance || dbg->want_top_weights)) {
         const size_t n = (size_t)c->src.n;
         if (c->dbg_cap < n) {
             dalloc(c->d_dbg_idx, n);
-            dalloc(c->d_dbg_w, n * d * d);
+            dalloc(c->d_dbg_w, n * 9);
             dalloc(c->d_dbg_dist, n);
+            dalloc(c->d_dbg_det, n);
             c->dbg_cap = n;
         }
-        a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
+        a.dbg_index = (dbg->index || dbg->want_top_weights) ? c->d_dbg_idx : nullptr;
         a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
         a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
+        if (dbg->want_top_weights) {   // rows of other shards stay NaN (never selected)
+            HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * n, st));
+            a.dbg_det = c->d_dbg_det;
+        }
     }
     const int nsx = nstat_ext(d);
     const int grid = corr_grid(c->q_end - c->q_begin, d);
@@ -694,6 +712,8 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     c->last_amb = c->h_stats[ns];
     c->last_pairs = c->h_stats[ns + 1];
     c->last_rebuilds = c->h_stats[ns + 2];
+    c->last_sq = c->h_stats[ns + 3];
+    c->top_ready = a.dbg_det != nullptr;
 }
 
 }  // namespace
@@ -787,6 +807,10 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_dbg_idx);
     dfree(c->d_dbg_w);
     dfree(c->d_dbg_dist);
+    dfree(c->d_dbg_det);
+    dfree(c->d_top_v);
+    dfree(c->d_top_i);
+    dfree(c->d_top_out);
     dfree(c->d_list);
     dfree(c->d_list_len);
     dfree(c->d_list_pass);
@@ -824,7 +848,8 @@ int gicp_comm_init(gicp_ctx* c, int nranks, int rank, const char id[GICP_COMM_ID
             ncclCommDestroy(c->comm);
             c->comm = nullptr;
         }
-        if (nranks == 1) return;
+        // a one-rank communicator is created too: the all-reduce then runs (as an identity) on the
+        // same stream path as a multi-GPU job, which is how the one-GPU tests exercise it
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof(uid));
         ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
@@ -838,6 +863,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
+        c->top_ready = false;
         build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, 0, 1, true);
         if (c->src.n) reset_tile_state(c);
     });
@@ -849,6 +875,7 @@ int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gi
     return guard_impl(c, "gicp_set_source", [&] {
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         c->psrc = resolve(dim, p);
+        c->top_ready = false;
         build_cloud(c, c->src, xyz, N, dim, c->psrc, shard, nshards, nshards == 1);
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -860,6 +887,7 @@ int gicp_target_to_source(gicp_ctx* c, int shard, int nshards) {
     return guard_impl(c, "gicp_target_to_source", [&] {
         if (!c->tgt.n) throw Fail{GICP_E_STATE, "no target to promote"};
         std::swap(c->src, c->tgt);   // the old source's buffers are kept for the next target
+        c->top_ready = false;
         c->tgt.n = 0;
         c->tgt.cov_ready = false;
         c->psrc = c->ptgt;
@@ -909,6 +937,41 @@ int gicp_iterate(gicp_ctx* c, const double* T, double* stats, gicp_debug* dbg) {
     });
 }
 
+int gicp_pass_info(gicp_ctx* c, double out[GICP_PASS_INFO]) {
+    if (!c || !out) return GICP_E_INVALID;
+    out[0] = c->last_amb;
+    out[1] = c->last_pairs;
+    out[2] = c->last_rebuilds;
+    out[3] = c->last_sq;
+    return GICP_OK;
+}
+
+int gicp_top_weights(gicp_ctx* c, int k, int64_t* src_out, int64_t* tgt_out, double* det_out) {
+    if (!c || k < 1 || k > 16) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_top_weights", [&] {
+        if (!c->top_ready) throw Fail{GICP_E_STATE, "no pass with want_top_weights since the last cloud change"};
+        constexpr int kBlocks = 256;
+        if (!c->d_top_v) {
+            dalloc(c->d_top_v, (size_t)kBlocks * 16 + 16);
+            dalloc(c->d_top_i, (size_t)kBlocks * 16);
+            dalloc(c->d_top_out, 32);
+        }
+        double* ov = c->d_top_v + (size_t)kBlocks * 16;
+        HIPCHK(launch_top_weights(c->d_dbg_det, c->d_dbg_idx, c->src.n, k, c->d_top_v, c->d_top_i, kBlocks, ov,
+                                  c->d_top_out, c->d_top_out + 16, c->stream));
+        std::vector<int64_t> hi(32);
+        std::vector<double> hv(16);
+        HIPCHK(hipMemcpyAsync(hi.data(), c->d_top_out, sizeof(int64_t) * 32, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hv.data(), ov, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int r = 0; r < k; ++r) {
+            if (src_out) src_out[r] = hi[r];
+            if (tgt_out) tgt_out[r] = hi[16 + r];
+            if (det_out) det_out[r] = hv[r];
+        }
+    });
+}
+
 int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_out, double* loss_out) {
     if ((dim != 2 && dim != 3) || !stats || !T_k || !T_out) return GICP_E_INVALID;
     try {
@@ -926,6 +989,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         const int d = c->src.dim, n1 = d + 1;
         gicp_params prm = p ? resolve(d, p) : c->psrc;
         c->psrc.max_distance_correspondence = prm.max_distance_correspondence;
+        c->psrc.cov_model = prm.cov_model;
         ensure_workspace(c);
         hipStream_t st = c->stream;
         // device state: T0, last_loss = inf (gicp.py:106-110)
@@ -937,6 +1001,11 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         hs.last_loss = INFINITY;
         hs.tol = prm.tolerance;
         hs.fixed = prm.fixed_iterations ? 1 : 0;
+        hs.trans_eps = prm.transformation_epsilon;
+        hs.rot_cos = prm.rotation_epsilon;
+        hs.fit_eps = prm.euclidean_fitness_epsilon;
+        hs.rel_eps = prm.mse_relative_epsilon;
+        hs.prev_mse = INFINITY;
         hs.converged_at = -1;
         HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
         const int grid = corr_grid(c->q_end - c->q_begin, d);
@@ -990,10 +1059,16 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             r.correspondences = (int64_t)hs.stats_solved[ns - 1];
             r.ambiguous = (int32_t)hs.stats_solved[ns];
             r.pairs_evaluated = (int64_t)hs.stats_solved[ns + 1];
+            c->last_amb = hs.stats_solved[ns];
+            c->last_pairs = hs.stats_solved[ns + 1];
+            c->last_rebuilds = hs.stats_solved[ns + 2];
+            c->last_sq = hs.stats_solved[ns + 3];
             r.wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
             // kernel time of the iterations actually executed (after convergence launches exit at once)
             r.corr_kernel_ms = samples ? corr_ms / samples * hs.iter : 0.0;
             r.reduce_ms = 0.0;
+            r.stop_reason = hs.converged ? hs.stop_reason : GICP_STOP_NONE;
+            r.mse = hs.mse;
             *res = r;
         }
     });

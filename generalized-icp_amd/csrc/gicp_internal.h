@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/gicp_hip.h"
+
 namespace gicp {
 
 constexpr int kWave = 64;          // CDNA wavefront
@@ -93,7 +95,14 @@ struct IterState {
     int32_t iter;             // outer iterations executed
     int32_t fixed;            // 1: never stop on tolerance (benchmark mode)
     int32_t solve_fail;
-    int32_t pad;
+    int32_t stop_reason;      // GICP_STOP_*
+    // PCL-style criteria (include/gicp_hip.h gicp_params; <= 0 disables), checked after the update
+    double trans_eps;         // |dt|^2 <= trans_eps and cos(angle) >= rot_cos of the increment
+    double rot_cos;
+    double fit_eps;           // |mse - prev_mse| < fit_eps
+    double rel_eps;           // |mse - prev_mse| / prev_mse < rel_eps
+    double prev_mse;          // +inf before the first pass
+    double mse;               // mean squared correspondence distance of the last solved pass
     double stats[80];         // statistics of the last pass (summed over ranks when a communicator is set)
     double stats_solved[80];  // copy of the statistics the last k_solve consumed (reporting)
 };
@@ -117,6 +126,9 @@ struct CorrArgs {
     int64_t* dbg_index;       // [N] original order (nullable)
     double* dbg_weight;       // [N][dim][dim] (nullable)
     double* dbg_dist;         // [N] (nullable)
+    double* dbg_det;          // [N] det(W), 0 if rejected, original order (nullable; gicp_top_weights)
+    int32_t cov_model;        // GICP_COV_* (include/gicp_hip.h)
+    double pl_inv;            // 1 / (epsilon (1 - ratio)): n n^T = m m^T * pl_inv (point-to-plane)
     int32_t count_pairs;      // 1: accumulate evaluated pairs (diagnostic)
     // per-source-tile candidate lists (certified): built by a full walk with the
     // search radius inflated by `skin`, reused while the tile's displacement since the build pose
@@ -143,7 +155,7 @@ struct CorrArgs {
 constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;
 }
-// partials carry two extra diagnostics: ambiguous count, pairs evaluated
-constexpr int nstat_ext(int D) { return nstat(D) + 3; }   // + ambiguous, pairs, list rebuilds
+// partials carry extra diagnostics: ambiguous count, pairs evaluated, list rebuilds, sum |r|^2
+constexpr int nstat_ext(int D) { return nstat(D) + 4; }
 
 }  // namespace gicp

@@ -985,7 +985,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     if (T >= A.q_end) T = -1;
     if (T >= 0) {
     bool on = false;          // accepted correspondence
-    double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0;
+    double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0, r2 = 0.0;
     bool amb = false;
     {
         const TileInfo st = tile_meta(sc, T);
@@ -1273,10 +1273,21 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = dist;
             if (!(dist > A.dc)) {  // gicp.py:136: reject only if distance > d_c
                 on = true;
-                const double4 cs = sc.cov[i];
                 const double4 ct = tg.cov[j];
-                const double ms[3] = {cs.y, cs.z, cs.w};
                 const double mt[3] = {ct.y, ct.z, ct.w};
+                if (A.cov_model == GICP_COV_POINT_TO_POINT) {          // C_s = 0, C_t = I: W = I
+#pragma unroll
+                    for (int a = 0; a < D; ++a)
+#pragma unroll
+                        for (int b = 0; b < D; ++b) W[a][b] = a == b ? 1.0 : 0.0;
+                } else if (A.cov_model == GICP_COV_POINT_TO_PLANE) {   // W = n_t n_t^T, n = m / |m|_model
+#pragma unroll
+                    for (int a = 0; a < D; ++a)
+#pragma unroll
+                        for (int b = 0; b < D; ++b) W[a][b] = mt[a] * mt[b] * A.pl_inv;
+                } else {
+                const double4 cs = sc.cov[i];
+                const double ms[3] = {cs.y, cs.z, cs.w};
                 double mr[D];
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
@@ -1311,9 +1322,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     W[1][2] = W[2][1] = c12 * id;
                     W[2][2] = c22 * id;
                 }
+                }   // plane-to-plane
                 double r[D];
 #pragma unroll
                 for (int a = 0; a < D; ++a) r[a] = qv[a] - q.p64[a];
+                r2 = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) r2 += r[a] * r[a];
                 rwr = 0.0;
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
@@ -1328,6 +1343,17 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = -1;
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = 1.0 / 0.0;
         }
+        if (A.dbg_det && q.valid) {   // det(W) for gicp_top_weights (gicp.py:170), 0 if rejected
+            double dt = 0.0;
+            if (on) {
+                if constexpr (D == 2) dt = W[0][0] * W[1][1] - W[0][1] * W[1][0];
+                else
+                    dt = W[0][0] * (W[1][1] * W[2][2] - W[1][2] * W[2][1]) -
+                         W[0][1] * (W[1][0] * W[2][2] - W[1][2] * W[2][0]) +
+                         W[0][2] * (W[1][0] * W[2][1] - W[1][1] * W[2][0]);
+            }
+            A.dbg_det[sc.perm[i]] = dt;
+        }
         if (A.dbg_weight && q.valid) {
             double* o = A.dbg_weight + (int64_t)sc.perm[i] * D * D;
 #pragma unroll
@@ -1338,6 +1364,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         amb = amb && q.valid;
     }
 
+    {   // sum |r|^2 of the accepted points (PCL's MSE numerator, extended slot): a plain wave sum here
+        // keeps r2 dead before the statistics GEMM (as a GEMM row it would cost 4 VGPRs and a wave/SIMD)
+        double t = on ? r2 : 0.0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if (l == 0) s_wstat[w][NSS + 3] += t;
+    }
     S.mark(5);
     // ---- wave reduction of the statistics: a 16x16x64 fp64 GEMM on MFMA ---------------------
     // stats[p][q] = sum over lanes of u_p v_q with u = (W sym, W r, r^T W r, 1), v = (s s sym, s, 1)
@@ -1773,14 +1806,175 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S) {
     S->iter = it + 1;
     if (!r.ok) S->solve_fail = 1;
     S->loss = r.loss;
+    constexpr int NSS = nstat(D);
+    const double cnt = S->stats[NSS - 1];
+    const double mse = cnt > 0.0 ? S->stats[NSS + 3] / cnt : 0.0;
+    S->mse = mse;
     if (!S->fixed && fabs(S->last_loss - r.loss) < S->tol) {   // gicp.py:160: stop before the update
         S->converged = 1;
         S->converged_at = it;
+        S->stop_reason = GICP_STOP_LOSS;
         return;
     }
     S->last_loss = r.loss;
+    // PCL-style criteria on the increment dT = T_new T_old^-1 and the pass's MSE; PCL applies the
+    // update and then tests, so these stop AFTER the update (include/gicp_hip.h GICP_STOP_*)
+    int reason = GICP_STOP_NONE;
+    if (!S->fixed) {
+        constexpr int N1 = D + 1;
+        double tr = 0.0, tsq = 0.0;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            double dta = r.T[a * N1 + D];
+#pragma unroll
+            for (int b = 0; b < D; ++b) {
+                double dr = 0.0;   // (R_new R_old^T)[a][b]
+#pragma unroll
+                for (int c = 0; c < D; ++c) dr += r.T[a * N1 + c] * S->T[b * N1 + c];
+                if (a == b) tr += dr;
+                dta -= dr * S->T[b * N1 + D];
+            }
+            tsq += dta * dta;
+        }
+        const double cosang = D == 3 ? 0.5 * (tr - 1.0) : 0.5 * tr;
+        const double dm = fabs(mse - S->prev_mse);
+        if (S->trans_eps > 0.0 && cosang >= S->rot_cos && tsq <= S->trans_eps) reason = GICP_STOP_TRANSFORM;
+        else if (S->fit_eps > 0.0 && dm < S->fit_eps) reason = GICP_STOP_ABS_MSE;
+        else if (S->rel_eps > 0.0 && dm / S->prev_mse < S->rel_eps) reason = GICP_STOP_REL_MSE;
+        S->prev_mse = mse;
+    }
 #pragma unroll
     for (int k = 0; k < (D + 1) * (D + 1); ++k) S->T[k] = r.T[k];
+    if (reason != GICP_STOP_NONE) {
+        S->converged = 1;
+        S->converged_at = it;
+        S->stop_reason = reason;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// top-k of det(W) for the drop-in's visualisation extras (gicp.py:169-172)
+// ---------------------------------------------------------------------------
+// Order: larger det first, equal dets -> larger original index first, i.e. the last k positions of a
+// stable ascending argsort.  NaN (rows of other ranks' shards, memset 0xFF) never enters a list.
+constexpr int kTopMax = 16;
+
+__device__ __forceinline__ bool top_gt(double va, int32_t ia, double vb, int32_t ib) {
+    return va > vb || (va == vb && ia > ib);
+}
+
+// Each thread keeps its k best in registers (descending, unrolled so nothing spills), then the block
+// pops its k best with k rounds of a block-wide argmax over the threads' heads.
+struct TopList {
+    double v[kTopMax];
+    int32_t i[kTopMax];
+    __device__ void init() {
+#pragma unroll
+        for (int p = 0; p < kTopMax; ++p) {
+            v[p] = -INFINITY;
+            i[p] = -1;
+        }
+    }
+    __device__ void insert(double cv, int32_t ci, int k) {
+        if (!top_gt(cv, ci, -INFINITY, -1)) return;   // NaN / sentinel
+#pragma unroll
+        for (int p = 0; p < kTopMax; ++p) {
+            if (p < k && top_gt(cv, ci, v[p], i[p])) {
+                const double tv = v[p];
+                const int32_t ti = i[p];
+                v[p] = cv;
+                i[p] = ci;
+                cv = tv;
+                ci = ti;
+            }
+        }
+    }
+};
+
+__device__ void top_block_emit(TopList& L, int k, double* out_v, int32_t* out_i) {
+    __shared__ double s_v[4];
+    __shared__ int32_t s_i[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int r = 0; r < k; ++r) {
+        double bv = L.v[0];
+        int32_t bi = L.i[0];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ov = __shfl_xor(bv, off);
+            const int32_t oi = __shfl_xor(bi, off);
+            if (top_gt(ov, oi, bv, bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        if (lane == 0) {
+            s_v[w] = bv;
+            s_i[w] = bi;
+        }
+        __syncthreads();
+        bv = s_v[0];
+        bi = s_i[0];
+        for (int u = 1; u < (int)(blockDim.x >> 6); ++u)
+            if (top_gt(s_v[u], s_i[u], bv, bi)) {
+                bv = s_v[u];
+                bi = s_i[u];
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            out_v[r] = bv;
+            out_i[r] = bi;
+        }
+        if (bi >= 0 && L.i[0] == bi && L.v[0] == bv) {   // indices are unique: exactly one owner pops
+#pragma unroll
+            for (int p = 0; p + 1 < kTopMax; ++p) {
+                L.v[p] = L.v[p + 1];
+                L.i[p] = L.i[p + 1];
+            }
+            L.v[kTopMax - 1] = -INFINITY;
+            L.i[kTopMax - 1] = -1;
+        }
+    }
+}
+
+// stage 1: block b reduces its contiguous chunk of det[0, n) to k candidates
+__global__ void __launch_bounds__(256) k_top1(const double* __restrict__ det, int64_t n, int k, double* pv, int32_t* pi) {
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = (int64_t)blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+    TopList L;
+    L.init();
+    for (int64_t x = b0 + threadIdx.x; x < b1; x += blockDim.x) L.insert(det[x], (int32_t)x, k);
+    top_block_emit(L, k, pv + (int64_t)blockIdx.x * k, pi + (int64_t)blockIdx.x * k);
+}
+
+// stage 2: one block merges the m = blocks x k candidates; ascending output (np.argsort(...)[-k:]),
+// plus the matched target index of each winner
+__global__ void __launch_bounds__(256) k_top2(const double* pv, const int32_t* pi, int m, int k,
+                                              const int64_t* __restrict__ tgt_index, double* ov, int64_t* osrc,
+                                              int64_t* otgt) {
+    __shared__ double s_ov[kTopMax];
+    __shared__ int32_t s_oi[kTopMax];
+    TopList L;
+    L.init();
+    for (int x = threadIdx.x; x < m; x += blockDim.x) L.insert(pv[x], pi[x], k);
+    top_block_emit(L, k, s_ov, s_oi);
+    __syncthreads();
+    if ((int)threadIdx.x < k) {
+        const int r = k - 1 - (int)threadIdx.x;   // descending -> ascending
+        const int32_t si = s_oi[r];
+        ov[threadIdx.x] = si >= 0 ? s_ov[r] : 0.0;
+        osrc[threadIdx.x] = si;
+        otgt[threadIdx.x] = si >= 0 ? tgt_index[si] : -1;
+    }
+}
+
+hipError_t launch_top_weights(const double* det, const int64_t* tgt_index, int64_t n, int k, double* scratch_v,
+                              int32_t* scratch_i, int blocks, double* ov, int64_t* osrc, int64_t* otgt,
+                              hipStream_t st) {
+    if (k < 1 || k > kTopMax || blocks < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_top1, dim3(blocks), dim3(256), 0, st, det, n, k, scratch_v, scratch_i);
+    hipLaunchKernelGGL(k_top2, dim3(1), dim3(256), 0, st, scratch_v, scratch_i, blocks * k, k, tgt_index, ov, osrc,
+                       otgt);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

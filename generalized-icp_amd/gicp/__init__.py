@@ -184,6 +184,27 @@ class Engine:
               "gicp_iterate")
         return (st, out) if debug else st
 
+    def pass_info(self):
+        """Diagnostics of the last pass: ambiguous lanes, pairs screened, list rebuilds, sum |r|^2."""
+        out = np.empty(_lib.PASS_INFO)
+        check(self._lib.gicp_pass_info(self._ctx, dptr(out)), self._ctx, "gicp_pass_info")
+        return dict(ambiguous=out[0], pairs=out[1], list_rebuilds=out[2], sum_sq=out[3])
+
+    def iterate_top(self, T, k=5):
+        """One pass at pose T keeping det(W) on the device, then its top-k on the device
+        (gicp.py:170 `np.argsort(det(W))[-k:]`): (statistics, src_idx[k], tgt_idx[k], det[k])."""
+        T = np.ascontiguousarray(np.asarray(T, dtype=np.float64))
+        st = np.empty(stats_size(self.dim))
+        dbg = Debug(None, None, None, 1)
+        check(self._lib.gicp_iterate(self._ctx, dptr(T), dptr(st), C.byref(dbg)), self._ctx, "gicp_iterate")
+        si = np.empty(k, dtype=np.int64)
+        ti = np.empty(k, dtype=np.int64)
+        dt = np.empty(k)
+        p64 = C.POINTER(C.c_int64)
+        check(self._lib.gicp_top_weights(self._ctx, k, si.ctypes.data_as(p64), ti.ctypes.data_as(p64), dptr(dt)),
+              self._ctx, "gicp_top_weights")
+        return st, si, ti, dt
+
     def align(self, T0=None, params=None):
         """The whole outer loop (gicp.py:116-167) natively; returns (T, result dict)."""
         d = self.dim
@@ -193,7 +214,10 @@ class Engine:
         p = params or default_params(d)
         check(self._lib.gicp_align(self._ctx, dptr(T0), C.byref(p), dptr(Tout), C.byref(res)), self._ctx,
               "gicp_align")
-        return Tout, res.as_dict()
+        r = res.as_dict()
+        r.pop("pad", None)
+        r["stop_reason"] = _lib.STOP_REASONS.get(r["stop_reason"], r["stop_reason"])
+        return Tout, r
 
 
 def solve_pose(stats, T_k):
@@ -271,9 +295,33 @@ def _engine(device):
     return eng
 
 
+def pcl_stop(T_old, T_new, mse, prev_mse, transformation_epsilon=0.0, rotation_epsilon=0.0,
+             euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
+    """PCL-style stopping test after an update (the criteria the reference's ROS experiment set,
+    presentation/main.typ:773-776; same order and semantics as k_solve): the increment
+    dT = T_new T_old^-1 with |dt|^2 <= transformation_epsilon and cos(angle) >= rotation threshold
+    (1 - transformation_epsilon when rotation_epsilon is 0), else |mse - prev| < euclidean_fitness_epsilon,
+    else |mse - prev| / prev < mse_relative_epsilon.  Returns 'transform' / 'abs_mse' / 'rel_mse' / None."""
+    d = T_old.shape[0] - 1
+    dR = T_new[:d, :d] @ T_old[:d, :d].T
+    dt = T_new[:d, d] - dR @ T_old[:d, d]
+    tr = float(np.trace(dR))
+    cosang = 0.5 * (tr - 1.0) if d == 3 else 0.5 * tr
+    rot_cos = rotation_epsilon if rotation_epsilon > 0 else 1.0 - transformation_epsilon
+    dm = abs(mse - prev_mse)
+    if transformation_epsilon > 0 and cosang >= rot_cos and float(dt @ dt) <= transformation_epsilon:
+        return "transform"
+    if euclidean_fitness_epsilon > 0 and dm < euclidean_fitness_epsilon:
+        return "abs_mse"
+    if mse_relative_epsilon > 0 and np.isfinite(prev_mse) and dm / prev_mse < mse_relative_epsilon:
+        return "rel_mse"
+    return None
+
+
 def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
          max_distance_nearest_neighbors=50, *, full_output=True, mode=None, inner=None, k_neighbors=None, device=0,
-         verbose=True, T0=None):
+         verbose=True, T0=None, method="plane_to_plane", transformation_epsilon=0.0, rotation_epsilon=0.0,
+         euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
     """Drop-in for gicp.py:78 — returns the same 7-tuple (gicp.py:174):
 
     (T, all_transformations, initial_source_cov_matrices, target_cov_matrices,
@@ -292,7 +340,14 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
       them -- by fmin_cg on the closed form (inner='cg', 2-D) or exactly by
       Newton on SO(d) (inner='newton').
     full_output=False skips the per-point visualisation extras (the three
-    lists come back empty), which is what large clouds want.
+    lists come back empty), which is what large clouds want.  In 'fast' mode the
+    top-5 det(W) points are selected on the GPU (no per-point copy).
+
+    method: 'plane_to_plane' (GICP, the reference), 'point_to_point' (ICP: C_s = 0,
+      C_t = I) or 'point_to_plane' (C_s = 0, C_t = P^-1), presentation/main.typ:446-455.
+    transformation_epsilon / rotation_epsilon / euclidean_fitness_epsilon /
+      mse_relative_epsilon: optional PCL-style stopping criteria (see pcl_stop), tested
+      after the update; 0 disables each.  tolerance=0 disables the reference's rule.
     """
     src = Engine._cloud(source_points)
     tgt = Engine._cloud(target_points)
@@ -305,10 +360,18 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     inner = ("cg" if d == 2 else "newton") if inner is None else inner
     if inner not in ("cg", "newton") or (inner == "cg" and d != 2):
         raise ValueError("inner must be 'newton', or 'cg' for 2-D clouds")
+    if method not in _lib.COV_MODELS:
+        raise ValueError(f"method must be one of {sorted(set(_lib.COV_MODELS))}")
     eng = _engine(device)
     p = default_params(d, max_iterations=int(max_iterations), tolerance=float(tolerance),
                        max_distance_correspondence=float(max_distance_correspondence),
-                       max_distance_nearest_neighbors=float(max_distance_nearest_neighbors), k_neighbors=k_neighbors)
+                       max_distance_nearest_neighbors=float(max_distance_nearest_neighbors), k_neighbors=k_neighbors,
+                       cov_model=_lib.COV_MODELS[method])
+    pcl = dict(transformation_epsilon=float(transformation_epsilon), rotation_epsilon=float(rotation_epsilon),
+               euclidean_fitness_epsilon=float(euclidean_fitness_epsilon),
+               mse_relative_epsilon=float(mse_relative_epsilon))
+    use_pcl = any(v > 0 for k, v in pcl.items() if k != "rotation_epsilon")
+    prev_mse = np.inf
     eng.set_target(tgt, p)
     target_cov = eng.covariances("target")
     eng.set_source(src, p)
@@ -339,7 +402,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
                 new_offset = None
         else:
             if full_output:
-                st, dbg = eng.iterate(T, debug=True)
+                st, top_s, top_t, _ = eng.iterate_top(T, 5)     # gicp.py:170 on the device
                 R = T[:d, :d]
                 all_src_cov.append(np.einsum("ab,nbc,dc->nad", R, init_src_cov, R))
             else:
@@ -356,15 +419,34 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
             break
         last = min_loss
         if full_output:                                            # gicp.py:169-172
-            idx = dbg["index"]
-            q = np.zeros_like(src)
-            q[idx >= 0] = tgt[idx[idx >= 0]]
-            top = np.argsort(np.linalg.det(dbg["weight"]))[-5:]
-            hw_s.append(moved[top])
-            hw_t.append(q[top])
+            if mode == "faithful":
+                idx = dbg["index"]
+                q = np.zeros_like(src)
+                q[idx >= 0] = tgt[idx[idx >= 0]]
+                top = np.argsort(np.linalg.det(dbg["weight"]))[-5:]
+                hw_s.append(moved[top])
+                hw_t.append(q[top])
+            else:
+                ok = top_s >= 0
+                qt = np.zeros((int(ok.sum()), d))
+                m = top_t[ok] >= 0
+                qt[m] = tgt[top_t[ok][m]]
+                hw_s.append(moved[top_s[ok]])
+                hw_t.append(qt)
         offset = new_offset
+        stop = None
+        if use_pcl:                                                # PCL-style criteria, after the update
+            info = eng.pass_info()
+            cnt = float(np.sum(dbg["index"] >= 0)) if mode == "faithful" else float(st[-1])
+            mse = info["sum_sq"] / cnt if cnt > 0 else 0.0
+            stop = pcl_stop(T, T_new, mse, prev_mse, **pcl)
+            prev_mse = mse
         T = T_new
         all_T.append(T)
+        if stop is not None:
+            if verbose:
+                print("Converged at iteration", it, f"({stop})")
+            break
     if mode == "faithful":
         eng.set_source(src, p)   # leave the engine holding the untransformed source
     return T, all_T, init_src_cov, target_cov, hw_s, hw_t, all_src_cov

@@ -21,6 +21,12 @@ GICP_E_STATE = -3
 GICP_E_COMM = -4
 GICP_E_NOMEM = -5
 COMM_ID_BYTES = 128
+PASS_INFO = 4
+
+# gicp_params.cov_model (include/gicp_hip.h GICP_COV_*)
+COV_MODELS = {"plane_to_plane": 0, "gicp": 0, "point_to_point": 1, "icp": 1, "point_to_plane": 2}
+# gicp_result.stop_reason (GICP_STOP_*)
+STOP_REASONS = {0: "none", 1: "loss", 2: "transform", 3: "abs_mse", 4: "rel_mse"}
 
 
 class Params(C.Structure):
@@ -35,6 +41,11 @@ class Params(C.Structure):
         ("ratio", C.c_double),
         ("fixed_iterations", C.c_int32),
         ("min_neighbors", C.c_int32),
+        ("cov_model", C.c_int32),
+        ("transformation_epsilon", C.c_double),
+        ("rotation_epsilon", C.c_double),
+        ("euclidean_fitness_epsilon", C.c_double),
+        ("mse_relative_epsilon", C.c_double),
     ]
 
 
@@ -50,6 +61,9 @@ class Result(C.Structure):
         ("corr_kernel_ms", C.c_double),
         ("reduce_ms", C.c_double),
         ("pairs_evaluated", C.c_int64),
+        ("stop_reason", C.c_int32),
+        ("pad", C.c_int32),
+        ("mse", C.c_double),
     ]
 
     def as_dict(self):
@@ -61,6 +75,7 @@ class Debug(C.Structure):
         ("index", C.POINTER(C.c_int64)),
         ("weight", C.POINTER(C.c_double)),
         ("distance", C.POINTER(C.c_double)),
+        ("want_top_weights", C.c_int32),
     ]
 
 
@@ -84,6 +99,8 @@ SIGNATURES = {
     "gicp_get_neighbor_counts": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int32)]),
     "gicp_iterate": (C.c_int, [_VP, _DP, _DP, C.POINTER(Debug)]),
     "gicp_solve_pose": (C.c_int, [C.c_int, _DP, _DP, _DP, _DP]),
+    "gicp_pass_info": (C.c_int, [_VP, _DP]),
+    "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
 }
 

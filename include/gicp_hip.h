@@ -56,12 +56,35 @@ typedef struct gicp_params {
     double ratio;                           /* 0.1 (gicp.py:11) */
     int32_t fixed_iterations;               /* 1: never stop on tolerance (benchmark mode) */
     int32_t min_neighbors;                  /* 0 -> dim (2-D: > 1 neighbour, gicp.py:27) */
+    /* --- additions beyond gicp.py; zero = the reference's behaviour --- */
+    int32_t cov_model;                      /* GICP_COV_* : which covariances weight a correspondence
+                                               (presentation/main.typ:446-455) */
+    double transformation_epsilon;          /* > 0: PCL-style stop when the iteration's increment has
+                                               |dt|^2 <= this and cos(angle) >= rotation threshold
+                                               (presentation/main.typ:773-776) */
+    double rotation_epsilon;                /* cosine threshold of that test; 0 -> 1 - transformation_epsilon
+                                               (PCL's default when its rotation epsilon is unset) */
+    double euclidean_fitness_epsilon;       /* > 0: stop when |MSE - previous MSE| < this, MSE = mean squared
+                                               correspondence distance of the pass (presentation/main.typ:776) */
+    double mse_relative_epsilon;            /* > 0: stop when |MSE - previous| / previous < this (PCL: 1e-5) */
 } gicp_params;
+
+/* gicp_params.cov_model (the GICP paper's three instances, presentation/main.typ:446-455) */
+#define GICP_COV_PLANE_TO_PLANE 0   /* W = inv(R C_s R^T + C_t), both surface covariances (gicp.py:143-145) */
+#define GICP_COV_POINT_TO_POINT 1   /* C_s = 0, C_t = I: W = I (standard ICP) */
+#define GICP_COV_POINT_TO_PLANE 2   /* C_s = 0, C_t = P^-1: W = n_t n_t^T (projection on the target normal) */
+
+/* gicp_result.stop_reason */
+#define GICP_STOP_NONE 0            /* max_iterations reached (or fixed_iterations) */
+#define GICP_STOP_LOSS 1            /* |delta loss| < tolerance, gicp.py:160 (the update is NOT applied) */
+#define GICP_STOP_TRANSFORM 2       /* transformation_epsilon test (the update IS applied, as PCL does) */
+#define GICP_STOP_ABS_MSE 3         /* euclidean_fitness_epsilon test (update applied) */
+#define GICP_STOP_REL_MSE 4         /* mse_relative_epsilon test (update applied) */
 
 /* What gicp_align() reports (the reference only prints "Converged at iteration", gicp.py:161). */
 typedef struct gicp_result {
     int32_t iterations;        /* outer iterations executed (each = correspondences + solve) */
-    int32_t converged;         /* 1 if |delta loss| < tolerance stopped the loop */
+    int32_t converged;         /* 1 if a stopping criterion ended the loop (which: stop_reason) */
     int32_t converged_at;      /* iteration index printed by gicp.py:161, -1 if none */
     int32_t ambiguous;         /* points re-resolved in fp64 in the last pass (diagnostic) */
     double final_loss;         /* min_loss of the last inner solve */
@@ -70,6 +93,9 @@ typedef struct gicp_result {
     double corr_kernel_ms;     /* correspondence-kernel time: mean HIP-event duration of every 8th launch x iterations */
     double reduce_ms;          /* sum of HIP-event durations of partial-reduce + all-reduce */
     int64_t pairs_evaluated;   /* source x target distance evaluations in the last pass (if counted) */
+    int32_t stop_reason;       /* GICP_STOP_* */
+    int32_t pad;
+    double mse;                /* mean squared correspondence distance of the last pass */
 } gicp_result;
 
 /* Optional caller-allocated per-point outputs of one pass, ORIGINAL source
@@ -78,6 +104,7 @@ typedef struct gicp_debug {
     int64_t* index;      /* [N] target index of the correspondence, -1 if rejected (gicp.py:136-138) */
     double* weight;      /* [N, dim, dim] W_i = inv(R C_s R^T + C_t), zeros if rejected (gicp.py:143-145) */
     double* distance;    /* [N] fp64 distance to the nearest target point (gicp.py:133) */
+    int32_t want_top_weights;  /* 1: the pass also keeps det(W) on the device for gicp_top_weights */
 } gicp_debug;
 
 /* ---- library ------------------------------------------------------------ */
@@ -122,6 +149,21 @@ int gicp_get_neighbor_counts(gicp_ctx* ctx, int which, int32_t* out);
  * gicp_stats_size(dim) doubles, summed over all ranks when a communicator is
  * set.  Layout: see DESIGN.md §4 (A, B, C, gR, gt, c0, count). */
 int gicp_iterate(gicp_ctx* ctx, const double* T, double* stats, gicp_debug* dbg);
+
+/* Per-pass diagnostics of the last gicp_iterate / gicp_align pass, summed over ranks:
+ * out[0] ambiguous lanes re-resolved in fp64, out[1] distance pairs screened, out[2] candidate-list
+ * rebuilds, out[3] sum of squared correspondence distances |q - (R s + t)|^2 (PCL's MSE numerator). */
+#define GICP_PASS_INFO 4
+int gicp_pass_info(gicp_ctx* ctx, double out[GICP_PASS_INFO]);
+
+/* The drop-in's visualisation extras (gicp.py:169-172) without copying per-point arrays: the k
+ * accepted source points of the last gicp_iterate pass with the largest det(W) (W as in
+ * gicp_debug.weight; rejected points have det 0), ascending by det as np.argsort(...)[-k:] yields
+ * them, ties broken towards the larger original index (the last k of a stable argsort).  Needs a
+ * preceding gicp_iterate whose gicp_debug had want_top_weights = 1.  src_out[k]: original source
+ * indices; tgt_out[k]: their matched target indices (-1 if rejected); det_out[k]: det(W).  Any
+ * output may be NULL.  1 <= k <= 16; slots beyond the shard's point count are -1 / 0. */
+int gicp_top_weights(gicp_ctx* ctx, int k, int64_t* src_out, int64_t* tgt_out, double* det_out);
 
 /* Host solve of the inner problem (gicp.py:148-154): minimise
  * c0 - 2 g^T dz + dz^T H dz over SE(dim), dz = z(T) - z(T_k), starting at T_k.

@@ -130,6 +130,64 @@ def weights(cov_src, cov_tgt, idx):
     return W
 
 
+def weights_model(cov_src, cov_tgt, idx, model="plane_to_plane", tgt_count=None, min_neighbors=None):
+    """The GICP paper's three covariance choices (reference slides presentation/main.typ:446-455):
+    plane_to_plane = gicp.py:143-145; point_to_point (standard ICP): C_s = 0, C_t = I -> W = I;
+    point_to_plane: C_s = 0, C_t = P^-1 -> W = P = n n^T, n the target's surface normal (eigenvector
+    of the smallest eigenvalue of its covariance), W = 0 where the target point has no surface
+    (fewer than min_neighbors neighbours: identity covariance, gicp.py:33-34)."""
+    if model in ("plane_to_plane", "gicp"):
+        return weights(cov_src, cov_tgt, idx)
+    n, d, _ = cov_src.shape
+    W = np.zeros((n, d, d))
+    ok = idx >= 0
+    if model in ("point_to_point", "icp"):
+        W[ok] = np.eye(d)
+        return W
+    if model != "point_to_plane":
+        raise ValueError(model)
+    _, vec = np.linalg.eigh(cov_tgt[idx[ok]])
+    nrm = vec[:, :, 0]
+    Wok = np.einsum("ni,nj->nij", nrm, nrm)
+    if tgt_count is not None:
+        mn = d if min_neighbors is None else min_neighbors
+        Wok[np.asarray(tgt_count)[idx[ok]] < mn] = 0.0
+    W[ok] = Wok
+    return W
+
+
+def mse(s, q, idx, T):
+    """Mean squared correspondence distance |q - (R s + t)|^2 over accepted points (PCL's
+    calculateMSE over the pass's correspondences; the euclidean-fitness criterion of the
+    reference's ROS experiment, presentation/main.typ:776)."""
+    d = s.shape[1]
+    ok = idx >= 0
+    if not ok.any():
+        return 0.0
+    r = q[ok] - s[ok] @ T[:d, :d].T - T[:d, d]
+    return float(np.mean(np.sum(r * r, axis=1)))
+
+
+def pcl_stop(T_old, T_new, mse_cur, mse_prev, transformation_epsilon=0.0, rotation_epsilon=0.0,
+             euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
+    """PCL DefaultConvergenceCriteria restated (transformation / absolute MSE / relative MSE, in that
+    order, max similar iterations 0), on the increment T_new T_old^-1; rotation threshold
+    1 - transformation_epsilon when unset.  The reference names these parameters
+    (presentation/main.typ:773-776, 802-805) but ships no implementation: parity unpinned by it."""
+    d = T_old.shape[0] - 1
+    inc = T_new @ np.linalg.inv(T_old)
+    cos_angle = 0.5 * (np.trace(inc[:d, :d]) - 1.0) if d == 3 else 0.5 * np.trace(inc[:d, :d])
+    tsq = float(np.sum(inc[:d, d] ** 2))
+    rot_thr = rotation_epsilon if rotation_epsilon > 0 else 1.0 - transformation_epsilon
+    if transformation_epsilon > 0 and cos_angle >= rot_thr and tsq <= transformation_epsilon:
+        return "transform"
+    if euclidean_fitness_epsilon > 0 and abs(mse_cur - mse_prev) < euclidean_fitness_epsilon:
+        return "abs_mse"
+    if mse_relative_epsilon > 0 and np.isfinite(mse_prev) and abs(mse_cur - mse_prev) / mse_prev < mse_relative_epsilon:
+        return "rel_mse"
+    return None
+
+
 # ---------------------------------------------------------------------------
 # loss and its sufficient statistics: gicp.py:52-76
 # ---------------------------------------------------------------------------
@@ -311,8 +369,12 @@ def inner_gn(s, q, W, idx, T0, max_iter=100, tol=1e-14):
 # ---------------------------------------------------------------------------
 def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
          max_distance_nearest_neighbors=50, inner=None, k=None, source_cov="auto", fixed_iterations=False,
-         record=False, T0=None):
+         record=False, T0=None, method="plane_to_plane", transformation_epsilon=0.0, rotation_epsilon=0.0,
+         euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
     """Oracle of gicp() returning the reference's 7-tuple (+ records if asked).
+
+    method / the PCL-style epsilons: the §8(f) extensions (weights_model, pcl_stop); defaults are the
+    reference's behaviour.
 
     inner: 'cg' (2-D default: scipy fmin_cg on the restated loss, reproducing
     the reference's inexact stopping), 'gn' (exact minimiser; 3-D default).
@@ -330,7 +392,12 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     if source_cov == "auto":
         source_cov = "recompute" if d == 2 else "rotate"
     d_c, d_n = max_distance_correspondence, max_distance_nearest_neighbors
-    tgt_cov, _ = covariances(tgt, d_n, k)
+    tgt_cov, tgt_cnt = covariances(tgt, d_n, k)
+    pcl = dict(transformation_epsilon=transformation_epsilon, rotation_epsilon=rotation_epsilon,
+               euclidean_fitness_epsilon=euclidean_fitness_epsilon, mse_relative_epsilon=mse_relative_epsilon)
+    use_pcl = transformation_epsilon > 0 or euclidean_fitness_epsilon > 0 or mse_relative_epsilon > 0
+    prev_mse = np.inf
+    stop_reason = None
     tree = cKDTree(tgt)
     T = np.eye(d + 1) if T0 is None else np.array(T0, dtype=np.float64)
     all_T = [T]
@@ -350,7 +417,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
         idx, dist = correspondences(moved, tgt, d_c, tree)
         q = np.zeros_like(src)
         q[idx >= 0] = tgt[idx[idx >= 0]]
-        W = weights(cs, tgt_cov, idx)
+        W = weights_model(cs, tgt_cov, idx, method, tgt_cnt)
         if inner == "cg":
             out = fmin_cg(f=lambda x: loss_2d(x, src, q, W), x0=offset,
                           fprime=lambda x: grad_2d(x, src, q, W), disp=False, full_output=True)
@@ -367,12 +434,19 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
             break
         last = min_loss
         offset = new_offset
+        if use_pcl and not fixed_iterations:
+            m = mse(src, q, idx, T)
+            stop_reason = pcl_stop(T, T_new, m, prev_mse, **pcl)
+            prev_mse = m
         T = T_new
         all_T.append(T)
         top = np.argsort(np.linalg.det(W))[-5:]                       # gicp.py:170-172
         hw_s.append(moved[top])
         hw_t.append(q[top])
+        if stop_reason is not None:
+            converged_at = it
+            break
     out = (T, all_T, init_src_cov, tgt_cov, hw_s, hw_t, all_src_cov)
     if record:
-        return out, dict(iterations=recs, converged_at=converged_at)
+        return out, dict(iterations=recs, converged_at=converged_at, stop_reason=stop_reason)
     return out

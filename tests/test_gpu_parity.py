@@ -256,3 +256,26 @@ def test_boundary_distances_exact(eng):
     cnt = eng.neighbor_counts("target")
     _, cnt_or = O.covariances(tgt, 4.0)
     assert list(cnt) == list(cnt_or)                # (0,0)-(0,4) at exactly 4: excluded
+
+
+def test_one_rank_rccl_allreduce_is_identity(scene3d):
+    """The RCCL all-reduce inside gicp_align/gicp_iterate (the multi-GPU exchange)
+    on a one-rank communicator: the library's stream path with the collective enqueued between
+    k_corr and k_solve must give bit-identical statistics and poses to the path without it."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=6, **P3)
+    res = []
+    for with_comm in (False, True):
+        e = gicp.Engine(0)
+        try:
+            if with_comm:
+                e.comm_init(1, 0, gicp.Engine.comm_unique_id())
+            e.set_target(tgt, p)
+            e.set_source(src, p)
+            st = e.iterate(np.eye(4))
+            T, r = e.align(None, p)
+            res.append((st, T, r["iterations"]))
+        finally:
+            e.close()
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1]) and res[0][2] == res[1][2] == 6
