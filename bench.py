@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--dim", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--shard-sim", type=int, default=1,
+                    help="diagnostic: one process runs only shard 0 of S (no collective) to time a rank of an "
+                         "S-GPU job; the line is marked and is not the metric")
     return ap.parse_args()
 
 
@@ -114,7 +117,10 @@ def main():
         eng.comm_init(world, rank, uid[0])
     t0 = time.perf_counter()
     eng.set_target(tgt, params)
-    eng.set_source(src, params, shard=rank, nshards=world)
+    if world == 1 and a.shard_sim > 1:
+        eng.set_source(src, params, shard=0, nshards=a.shard_sim)
+    else:
+        eng.set_source(src, params, shard=rank, nshards=world)
     setup_ms = (time.perf_counter() - t0) * 1e3
 
     def sync():
@@ -140,11 +146,11 @@ def main():
         return
     from gicp.synthetic import rotation_angle_error, translation_error
     rot_err, tr_err = rotation_angle_error(T, Tgt), translation_error(T, Tgt)
-    n_shard = a.n / world
+    n_shard = a.n / max(world, a.shard_sim)
     corr_avg_ms = res["corr_kernel_ms"] / a.steps
     alg_bytes = BYTES_PER_POINT * (n_shard + a.n)
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
-    pairs = res["pairs_evaluated"] / world
+    pairs = res["pairs_evaluated"] / world   # summed over ranks by the all-reduce
     traffic, traffic_src = measured_traffic(name) if world == 1 else (None, None)
     line = {
         "metric": "GICP iterations/sec (and ms/iter) at N points, 1/2/4/8 GPU; final transform error",
@@ -173,6 +179,11 @@ def main():
         "correspondences": res["correspondences"],
         "ambiguous_last_pass": res["ambiguous"],
     }
+    if a.shard_sim > 1 and world == 1:
+        line["diagnostic"] = f"shard 0 of {a.shard_sim} only, no all-reduce: one rank of a {a.shard_sim}-GPU job"
+        line["cpu_baseline"] = None
+        print(json.dumps(line))
+        return
     if world == 1 and not a.no_cpu_baseline:
         try:
             its, setup, dt = cpu_baseline(src, tgt, kw, a.cpu_workers)

@@ -179,6 +179,13 @@ struct gicp_ctx {
     int32_t* d_list_pass = nullptr;
     float* d_list_rcert = nullptr;
     double* d_poses = nullptr;
+    // per-source-point nearest-neighbour certificates
+    int32_t* d_cert_j = nullptr;
+    float* d_cert_gap = nullptr;
+    int32_t* d_cert_pass = nullptr;
+    size_t cap_cj = 0, cap_cg = 0, cap_cp = 0;
+    bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
+    double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     // cloud-build scratch and per-source-tile arrays, grow-only (a frame stream allocates once)
     double* s_in = nullptr;
     uint32_t *s_codes = nullptr, *s_codes2 = nullptr;
@@ -509,6 +516,7 @@ void reset_tile_state(gicp_ctx* c) {
     HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
     HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
     HIPCHK(hipMemsetAsync(c->d_order_cnt, 0, sizeof(int32_t) * 2 * 8 * kOrderBuckets, c->stream));
+    if (c->d_cert_pass) HIPCHK(hipMemsetAsync(c->d_cert_pass, 0xFF, sizeof(int32_t) * nt, c->stream));
     c->pass = 0;
 }
 
@@ -525,6 +533,9 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     dreserve(c->d_list_pass, c->cap_lpass, nt);
     dreserve(c->d_list_rcert, c->cap_lrc, nt);
     if (!c->d_poses) dalloc(c->d_poses, (size_t)kPoseRing * 12);
+    dreserve(c->d_cert_j, c->cap_cj, (size_t)std::max<int64_t>(1, c->src.n));
+    dreserve(c->d_cert_gap, c->cap_cg, (size_t)std::max<int64_t>(1, c->src.n));
+    dreserve(c->d_cert_pass, c->cap_cp, nt);
     const int q8 = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim) / 8);
     dreserve(c->d_order, c->cap_order, (size_t)2 * 8 * kOrderBuckets * q8);
     if (!c->d_order_cnt) dalloc(c->d_order_cnt, 2 * 8 * kOrderBuckets);
@@ -564,8 +575,17 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.single_pass = single_pass;
     const double dc = c->psrc.max_distance_correspondence;
     a.dc = dc;
-    a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc);
-    a.search2 = screen_bound(a.mg, dc);
+    // with certificates the screen reaches kappa past d_c, so an empty lane's radius outlasts small moves
+    const double kappa = c->use_certs ? c->kappa_frac * dc : 0.0;
+    a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc + kappa);
+    a.search2 = screen_bound(a.mg, dc + kappa);
+    a.kappa = (float)kappa;
+    a.empty_r = (float)dc * (1.0f + 1e-6f);
+    if (c->use_certs) {
+        a.cert_j = c->d_cert_j;
+        a.cert_gap = c->d_cert_gap;
+        a.cert_pass = c->d_cert_pass;
+    }
     a.hint = c->d_hint;
     a.order = c->use_order ? c->d_order : nullptr;
     a.order_cnt = c->d_order_cnt;
@@ -768,6 +788,8 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_NO_ORDER")) c->use_order = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
+    if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;
@@ -808,6 +830,9 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_dbg_w);
     dfree(c->d_dbg_dist);
     dfree(c->d_dbg_det);
+    dfree(c->d_cert_j);
+    dfree(c->d_cert_gap);
+    dfree(c->d_cert_pass);
     dfree(c->d_top_v);
     dfree(c->d_top_i);
     dfree(c->d_top_out);

@@ -141,6 +141,12 @@ struct CorrArgs {
     int32_t pass;             // this pass's id (monotonic per source cloud)
     int32_t use_lists;        // 0: always full walk (no lists)
     float skin;
+    // per-source-point nearest-neighbour certificates, sorted source order; null: off
+    int32_t* cert_j;          // [src.n] sorted target index of the certified nearest, -1: none within R
+    float* cert_gap;          // [src.n] runner-up gap (found) or empty radius R (none), relative to cert_pass
+    int32_t* cert_pass;       // [src.ntiles] pass the tile's certificates refer to (-1: none)
+    float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
+    float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected
     unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
     // longest-first order: a UNIT is the kCorrWaves consecutive source tiles one
     // workgroup handles; its partial row and reduction group follow the unit, so the statistics do

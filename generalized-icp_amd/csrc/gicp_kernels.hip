@@ -947,7 +947,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     if (A.stamps && l == 0)   // stored at once: no register held across the wave
         A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 20 + 16] = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (A.use_lists && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
+    if ((A.use_lists || A.cert_j) && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
         double* ring = A.poses + (A.pass % kPoseRing) * 12;
         for (int a = 0; a < 3; ++a) {
             for (int b = 0; b < 3; ++b) ring[a * 3 + b] = (a < D && b < D) ? P.R[a * D + b] : 0.0;
@@ -1023,14 +1023,57 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             seed = lo;
         }
 
+        // displacement bound of any point of this source tile between the pose of pass `bp` (pose ring)
+        // and this pass: |dR c + dt| + ||dR||_F rho; < 0 if that pose has left the ring
+        auto disp_since = [&](int bp) -> float {
+            if (bp < 0 || A.pass - bp <= 0 || A.pass - bp >= kPoseRing) return -1.f;
+            const double* Pb = A.poses + (bp % kPoseRing) * 12;
+            double dc2 = 0.0, dr2 = 0.0;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                double m = P.t[a] - Pb[9 + a];
+#pragma unroll
+                for (int b = 0; b < D; ++b) {
+                    const double dr = P.R[a * D + b] - Pb[a * 3 + b];
+                    m += dr * st.c[b];
+                    dr2 += dr * dr;
+                }
+                dc2 += m * m;
+            }
+            return (float)(sqrt(dc2) + sqrt(dr2) * (double)st.radius) * 1.0001f + 1e-30f;
+        };
+
+        // ---- per-point nearest-neighbour certificates ------------------------
+        // A lane whose last scan proved "target j is nearest and every other target is >= gap farther"
+        // (or "no target within R") keeps that answer while its displacement since then, delta, obeys
+        // 2 delta < gap (R - delta > d_c: still rejected, gicp.py:136): d(p', j) <= d1 + delta < d2 - delta <= d(p', k).
+        // Certified lanes take no part in the walk; a wave whose lanes are all certified skips it.
+        bool cert = false;
+        int cj = -1;
+        float cgap = 0.f, cdelta = -1.f;
+        if (A.cert_j) {
+            cdelta = disp_since(A.cert_pass[T]);
+            if (cdelta >= 0.f && q.valid) {
+                cj = A.cert_j[i];
+                cgap = A.cert_gap[i];
+                cert = cj >= 0 ? 2.f * cdelta < cgap : cgap - cdelta > A.empty_r;
+            }
+        }
+        const bool skip_walk = !wave_any(q.valid && !cert);
+
         // ---- fp32 screen: best and runner-up keys -------------------------
         const unsigned init = __float_as_uint(A.search2) | 63u;
         unsigned best = init, sec = init;
         int best_tile = -1;
+        // lane search bound: the runner-up, or the winner plus the screen's ambiguity band, widened to
+        // (sqrt(b) + kappa)^2 when certificates are kept so the runner-up gap is known up to kappa
         auto lane_bound = [&]() -> float {
-            if (!q.valid) return -1.f;
+            if (!q.valid || cert) return -1.f;
             const float b = key_d2(best);
-            return fminf(key_d2(sec), b + 2.f * marg(A.mg, b));
+            float w = b + 2.f * marg(A.mg, b);
+            const float r = __builtin_amdgcn_sqrtf(b) + A.kappa;
+            w = fmaxf(w, r * r);
+            return fminf(key_d2(sec), w);
         };
         float lb = lane_bound();   // refreshed after every merge
         // lb inflated by the rounding slack, for the slack-free box tests
@@ -1083,26 +1126,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         bool use = false;
         float delta = 0.f, rc = 0.f;
         int nl = 0;
-        if (lists) {
+        if (lists && !skip_walk) {
             nl = A.list_len[T];
             rc = A.list_rcert[T];
-            const int bp = A.list_pass[T];
-            if (nl > 0 && rc > 0.f && A.pass - bp > 0 && A.pass - bp < kPoseRing) {
-                const double* Pb = A.poses + (bp % kPoseRing) * 12;
-                double dc2 = 0.0, dr2 = 0.0;
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    double m = P.t[a] - Pb[9 + a];
-#pragma unroll
-                    for (int b = 0; b < D; ++b) {
-                        const double dr = P.R[a * D + b] - Pb[a * 3 + b];
-                        m += dr * st.c[b];
-                        dr2 += dr * dr;
-                    }
-                    dc2 += m * m;
-                }
-                delta = (float)(sqrt(dc2) + sqrt(dr2) * (double)st.radius) * 1.0001f + 1e-30f;
-                use = delta < rc;
+            if (nl > 0 && rc > 0.f) {
+                delta = disp_since(A.list_pass[T]);
+                use = delta >= 0.f && delta < rc;
             }
         }
         int ent = 0;   // lane k: list entry k (when the list is used)
@@ -1154,7 +1183,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 ++list_rebuilds;
             }
         }
-        if (!use) {
+        if (!use && !skip_walk) {
             int ncol = 0;
             int cent = 0x7fffffff;   // lane k: collected entry k
             auto collect = [&](int Tt) {
@@ -1201,16 +1230,38 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 sv[a] = s4v[a];
             }
         }
-        const bool found = q.valid && best < init;
+        const bool found = cert ? cj >= 0 : (q.valid && best < init);
         int j = -1;
         double d2e = 0.0;
-        if (found) {
+        if (cert) {
+            j = cj;
+        } else if (found) {
             const float b = key_d2(best), s2 = key_d2(sec);
             amb = (s2 - b) <= marg(A.mg, b) + marg(A.mg, s2);
             j = tg.tiles[best_tile].start + (int)(best & 63u);
         }
+        if (A.cert_j) {   // every lane's certificate is restated relative to this pass's pose
+            if (q.valid) {
+                float g = 0.f;
+                if (cert) {
+                    g = cj >= 0 ? cgap - 2.f * cdelta : cgap - cdelta;
+                } else if (found) {
+                    if (!amb) {   // other targets: scanned >= sec - margin, unscanned > the final bound
+                        const float b = key_d2(best), s2 = key_d2(sec);
+                        const float lo2 = fminf(s2 - marg(A.mg, s2), lane_bound());
+                        const float hi2 = b + marg(A.mg, b);
+                        g = (__builtin_amdgcn_sqrtf(fmaxf(lo2, 0.f)) - __builtin_amdgcn_sqrtf(hi2)) * 0.999f;
+                    }
+                } else {   // nothing within the screen radius: every target's d^2 >= search2 - margin
+                    g = __builtin_amdgcn_sqrtf(A.search2 - marg(A.mg, A.search2)) * 0.9999f;
+                }
+                A.cert_j[i] = cert ? cj : (found && !amb ? j : -1);
+                A.cert_gap[i] = (found && amb) ? 0.f : g;
+            }
+            if (l == 0) A.cert_pass[T] = A.pass;
+        }
         // hint for the next pass: the first lane's winning tile
-        const uint64_t fm = __ballot(found);
+        const uint64_t fm = __ballot(found && !cert);
         if (fm && A.hint) {
             const int src_lane = __ffsll((unsigned long long)fm) - 1;
             const int bt = __shfl(best_tile, src_lane);

@@ -31,3 +31,7 @@ T, res = eng.align(None, p)
 print("== steady state (after %d iterations)" % a.iters, file=sys.stderr, flush=True)
 eng.iterate(T)
 eng.iterate(T)
+print("== early (after 2 iterations from identity, fresh lists)", file=sys.stderr, flush=True)
+p.max_iterations = 2
+T2, _ = eng.align(None, p)
+eng.iterate(T2)

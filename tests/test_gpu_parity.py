@@ -279,3 +279,34 @@ def test_one_rank_rccl_allreduce_is_identity(scene3d):
             e.close()
     assert np.array_equal(res[0][0], res[1][0])
     assert np.array_equal(res[0][1], res[1][1]) and res[0][2] == res[1][2] == 6
+
+
+def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
+    """Per-point nearest-neighbour certificates skip the walk for lanes whose nearest
+    target is provably unchanged: a 60-iteration fixed run and single passes around its endpoint must
+    be bit-identical to an engine without them (GICP_NO_CERTS=1), while the certified passes evaluate
+    far fewer pairs."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GICP_NO_CERTS", flag)
+        e = gicp.Engine(0)
+        try:
+            e.set_target(tgt, p)
+            e.set_source(src, p)
+            T, r = e.align(None, p)
+            sts = [e.iterate(T), e.iterate(T)]
+            Tn = T.copy()
+            Tn[:3, 3] += [1e-4, -2e-4, 5e-5]          # a small move: most certificates still hold
+            sts.append(e.iterate(Tn))
+            Tf = T.copy()
+            Tf[:3, 3] += [0.2, 0.0, 0.0]              # a large one: they must not
+            sts.append(e.iterate(Tf))
+            out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
+        finally:
+            e.close()
+    assert np.array_equal(out["0"][0], out["1"][0])
+    for a, b in zip(out["0"][1], out["1"][1]):
+        assert np.array_equal(a, b)
+    assert out["0"][3] < 0.05 * out["1"][3]            # the converged pass walked almost nothing
