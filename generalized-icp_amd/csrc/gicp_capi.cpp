@@ -1031,6 +1031,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         hs.fit_eps = prm.euclidean_fitness_epsilon;
         hs.rel_eps = prm.mse_relative_epsilon;
         hs.prev_mse = INFINITY;
+        hs.pairs_total = 0.0;
         hs.converged_at = -1;
         HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
         const int grid = corr_grid(c->q_end - c->q_begin, d);
@@ -1040,7 +1041,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         int enq = 0, samples = 0;
         // Timing events are recorded around every kEvStride-th k_corr only: an event pair around
         // every launch inserts a few microseconds of queue work per iteration.
-        constexpr int kEvStride = 8;
+        const int kEvStride = prm.timing_stride > 0 ? std::min(prm.timing_stride, (int)gicp_ctx::kMaxBatch) : 8;
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
         // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
         // After convergence the remaining launches of a batch exit at once.
@@ -1093,6 +1094,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             r.corr_kernel_ms = samples ? corr_ms / samples * hs.iter : 0.0;
             r.reduce_ms = 0.0;
             r.stop_reason = hs.converged ? hs.stop_reason : GICP_STOP_NONE;
+            r.pairs_total = hs.pairs_total;
             r.mse = hs.mse;
             *res = r;
         }

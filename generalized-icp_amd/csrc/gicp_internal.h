@@ -103,6 +103,7 @@ struct IterState {
     double rel_eps;           // |mse - prev_mse| / prev_mse < rel_eps
     double prev_mse;          // +inf before the first pass
     double mse;               // mean squared correspondence distance of the last solved pass
+    double pairs_total;       // distance pairs screened, summed over the passes k_solve consumed
     double stats[80];         // statistics of the last pass (summed over ranks when a communicator is set)
     double stats_solved[80];  // copy of the statistics the last k_solve consumed (reporting)
 };

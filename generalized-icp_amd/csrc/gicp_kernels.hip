@@ -1858,6 +1858,7 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S) {
     if (!r.ok) S->solve_fail = 1;
     S->loss = r.loss;
     constexpr int NSS = nstat(D);
+    S->pairs_total += S->stats[NSS + 1];
     const double cnt = S->stats[NSS - 1];
     const double mse = cnt > 0.0 ? S->stats[NSS + 3] / cnt : 0.0;
     S->mse = mse;

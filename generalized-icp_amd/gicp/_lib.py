@@ -41,6 +41,7 @@ class Params(C.Structure):
         ("ratio", C.c_double),
         ("fixed_iterations", C.c_int32),
         ("min_neighbors", C.c_int32),
+        ("timing_stride", C.c_int32),
         ("cov_model", C.c_int32),
         ("transformation_epsilon", C.c_double),
         ("rotation_epsilon", C.c_double),
@@ -64,6 +65,7 @@ class Result(C.Structure):
         ("stop_reason", C.c_int32),
         ("pad", C.c_int32),
         ("mse", C.c_double),
+        ("pairs_total", C.c_double),
     ]
 
     def as_dict(self):

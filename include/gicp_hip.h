@@ -56,6 +56,8 @@ typedef struct gicp_params {
     double ratio;                           /* 0.1 (gicp.py:11) */
     int32_t fixed_iterations;               /* 1: never stop on tolerance (benchmark mode) */
     int32_t min_neighbors;                  /* 0 -> dim (2-D: > 1 neighbour, gicp.py:27) */
+    int32_t timing_stride;                  /* gicp_align times every n-th correspondence launch with HIP
+                                               events (0 -> 8; 1 = every launch, adds queue work) */
     /* --- additions beyond gicp.py; zero = the reference's behaviour --- */
     int32_t cov_model;                      /* GICP_COV_* : which covariances weight a correspondence
                                                (presentation/main.typ:446-455) */
@@ -96,6 +98,7 @@ typedef struct gicp_result {
     int32_t stop_reason;       /* GICP_STOP_* */
     int32_t pad;
     double mse;                /* mean squared correspondence distance of the last pass */
+    double pairs_total;        /* distance pairs screened over all passes of this call, all ranks */
 } gicp_result;
 
 /* Optional caller-allocated per-point outputs of one pass, ORIGINAL source
