@@ -1042,6 +1042,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         // Timing events are recorded around every kEvStride-th k_corr only: an event pair around
         // every launch inserts a few microseconds of queue work per iteration.
         const int kEvStride = prm.timing_stride > 0 ? std::min(prm.timing_stride, (int)gicp_ctx::kMaxBatch) : 8;
+        const int kEvOffset = std::max(0, prm.timing_offset) % kEvStride;
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
         // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
         // After convergence the remaining launches of a batch exit at once.
@@ -1050,7 +1051,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
                                    prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 4);
             for (int b = 0; b < B; ++b) {
                 CorrArgs a = corr_args(c, 0);
-                const bool ev = timing && b % kEvStride == 0;
+                const bool ev = timing && (enq + b) % kEvStride == kEvOffset;
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b], st));
                 if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
                 else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nstat_ext(d), st));
@@ -1062,7 +1063,8 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             HIPCHK(hipMemcpyAsync(&hs, c->d_state, sizeof(IterState), hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             if (timing)
-                for (int b = 0; b < B; b += kEvStride) {
+                for (int b = 0; b < B; ++b) {
+                    if ((enq - B + b) % kEvStride != kEvOffset) continue;
                     if (enq - B + b >= hs.iter) break;   // launched after convergence: exited at once
                     float ms = 0.f;
                     HIPCHK(hipEventElapsedTime(&ms, c->ev[2 * b], c->ev[2 * b + 1]));
@@ -1095,6 +1097,8 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             r.reduce_ms = 0.0;
             r.stop_reason = hs.converged ? hs.stop_reason : GICP_STOP_NONE;
             r.pairs_total = hs.pairs_total;
+            r.corr_kernel_ms_sampled = corr_ms;
+            r.corr_samples = samples;
             r.mse = hs.mse;
             *res = r;
         }

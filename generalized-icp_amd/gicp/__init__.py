@@ -216,6 +216,7 @@ class Engine:
               "gicp_align")
         r = res.as_dict()
         r.pop("pad", None)
+        r.pop("pad2", None)
         r["stop_reason"] = _lib.STOP_REASONS.get(r["stop_reason"], r["stop_reason"])
         return Tout, r
 

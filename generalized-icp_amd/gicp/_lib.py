@@ -42,6 +42,7 @@ class Params(C.Structure):
         ("fixed_iterations", C.c_int32),
         ("min_neighbors", C.c_int32),
         ("timing_stride", C.c_int32),
+        ("timing_offset", C.c_int32),
         ("cov_model", C.c_int32),
         ("transformation_epsilon", C.c_double),
         ("rotation_epsilon", C.c_double),
@@ -66,6 +67,9 @@ class Result(C.Structure):
         ("pad", C.c_int32),
         ("mse", C.c_double),
         ("pairs_total", C.c_double),
+        ("corr_kernel_ms_sampled", C.c_double),
+        ("corr_samples", C.c_int32),
+        ("pad2", C.c_int32),
     ]
 
     def as_dict(self):

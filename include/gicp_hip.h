@@ -57,7 +57,8 @@ typedef struct gicp_params {
     int32_t fixed_iterations;               /* 1: never stop on tolerance (benchmark mode) */
     int32_t min_neighbors;                  /* 0 -> dim (2-D: > 1 neighbour, gicp.py:27) */
     int32_t timing_stride;                  /* gicp_align times every n-th correspondence launch with HIP
-                                               events (0 -> 8; 1 = every launch, adds queue work) */
+                                               events (0 -> 8; 1 = every launch, adds queue work) ... */
+    int32_t timing_offset;                  /* ... starting at launch timing_offset (< stride) */
     /* --- additions beyond gicp.py; zero = the reference's behaviour --- */
     int32_t cov_model;                      /* GICP_COV_* : which covariances weight a correspondence
                                                (presentation/main.typ:446-455) */
@@ -99,6 +100,9 @@ typedef struct gicp_result {
     int32_t pad;
     double mse;                /* mean squared correspondence distance of the last pass */
     double pairs_total;        /* distance pairs screened over all passes of this call, all ranks */
+    double corr_kernel_ms_sampled;  /* sum of the event-timed correspondence launches ... */
+    int32_t corr_samples;           /* ... and how many there were */
+    int32_t pad2;
 } gicp_result;
 
 /* Optional caller-allocated per-point outputs of one pass, ORIGINAL source
