@@ -871,8 +871,9 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 #define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(GICP_CORR_WAVES_PER_EU, GICP_CORR_WAVES_PER_EU)))
 #elif defined(GICP_TIMELINE)   // keep the diagnostic build at the product's 7 waves per SIMD
 #define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(7, 7)))
-#else
-#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR)))
+#else   // 7 waves per SIMD: at 73 VGPRs the allocator would settle for 6; held to 72 it spills one
+        // double once per wave (stored in the prologue, reloaded for the statistics)
+#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(7, 7)))
 #endif
 #endif
 #ifndef GICP_CORR_SGPR
@@ -1270,8 +1271,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
         // ---- fp64 re-resolution of the lanes the screen could not decide ----
         if (__any(amb)) {
-            double bd2 = 1e300;
-            int bj = -1, bo = 0x7FFFFFFF;
+            double bd2 = 1e300;   // exact best d^2 among the rows scanned
+            float sd2 = 3e38f;    // runner-up d^2, rounded down (a lower bound is all a certificate needs)
+            int bj = -1;   // its sorted index; the original index (tie-break) is read only on exact ties
             const float lim = key_d2(best) + 2.f * marg(A.mg, key_d2(best));
             auto visit64 = [&](int Tt) -> bool {
                 const TileInfo ti = tile_meta(tg, Tt);
@@ -1291,10 +1293,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         const double qq[3] = {L.t.x64[jj], L.t.y64[jj], L.t.z64[jj]};
                         const double d2 = dist2_exact<D>(qq, q.p64);
                         const int og = L.t.perm[jj];
-                        if (amb && (d2 < bd2 || (d2 == bd2 && og < bo))) {
-                            bd2 = d2;
-                            bj = ti.start + jj;
-                            bo = og;
+                        if (amb) {
+                            if (d2 < bd2 || (d2 == bd2 && bj >= 0 && og < tg.perm[bj])) {
+                                sd2 = (float)bd2 * 0.99999976f;
+                                bd2 = d2;
+                                bj = ti.start + jj;
+                            } else {
+                                sd2 = fminf(sd2, (float)d2 * 0.99999976f);
+                            }
                         }
                     }
                 }
@@ -1312,6 +1318,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
             }
             if (amb) j = bj;
+            // exact certificate of a re-resolved lane: every row within lim was scanned in fp64, so
+            // each other target lies at d^2 >= min(runner-up, lim); a near tie certifies only while
+            // the pose moves by less than half its (tiny, possibly zero) gap
+            if (A.cert_j && amb) {
+                const double g = (sqrt((double)fminf(sd2, lim)) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
+                A.cert_j[i] = bj;
+                A.cert_gap[i] = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
+            }
         }
 
         S.mark(4);
