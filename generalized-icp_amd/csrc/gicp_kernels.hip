@@ -1641,8 +1641,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 // (H' dr, H' D_l, the loss) are lane-parallel and meet through LDS; the small dense work
 // (the M x M Newton system, the rotation update) runs redundantly in every lane, which keeps
 // the control flow uniform. Same iterates as the serial solver up to summation order.
-template <int D>
-__device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
+template <int D, class Sync>
+__device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync sync) {
     using namespace solver_detail;
     constexpr int NS = D * (D + 1) / 2, NR = D * D, N1 = D + 1, M = D == 2 ? 1 : 3;
     __shared__ double s_kc[D][NR], s_u[NR], s_hd[M][NR], s_f[NR];
@@ -1692,7 +1692,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
 #pragma unroll
             for (int a = 0; a < D; ++a) s_kc[a][lane] = x[a];
     }
-    __syncthreads();
+    sync();
     // row i of H' and g'_i
     double Hrow[NR], gpi;
     {
@@ -1726,11 +1726,11 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
         }
         ui = hi - gpi;
         if (lane < NR) s_f[lane] = dri * hi - 2.0 * gpi * dri;
-        __syncthreads();
+        sync();
         double f = c0p;
 #pragma unroll
         for (int j = 0; j < NR; ++j) f += s_f[j];
-        __syncthreads();
+        sync();
         return f;
     };
 
@@ -1754,7 +1754,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
                 s_hd[l][lane] = s;
             }
         }
-        __syncthreads();
+        sync();
         // grad_k = 2 u.vec(G_k R) and the second-order term u.vec(1/2 (G_k G_l + G_l G_k) R) of the
         // serial solver, through P = R U^T (U = u as a D x D matrix): u.vec(X R) = tr(X P),
         // G_k G_l = e_l e_k^T - delta_kl I in 3-D and G^2 = -I in 2-D.
@@ -1789,7 +1789,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
                 const double t2 = D == 2 ? -trP : 0.5 * (P[k][l] + P[l][k]) - (k == l ? trP : 0.0);
                 Hs[k][l] = Hs[l][k] = 2.0 * s + 2.0 * t2;
             }
-        __syncthreads();   // s_u / s_hd are rewritten next iteration
+        sync();   // s_u / s_hd are rewritten next iteration
         double gmax = 0.0, hscale = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -1855,26 +1855,26 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk) {
     return out;
 }
 
-// One wave: the inner solve (gicp.py:148-154) from the pass's statistics, then the convergence
-// test and pose update of gicp.py:155-167, all on the device so iterations need no host sync.
-template <int D>
-__global__ void __launch_bounds__(64) k_solve(IterState* S) {
-    if (S->converged) return;
-    const int lane = threadIdx.x;
+// The inner solve (gicp.py:148-154) from a pass's statistics `st`, then the convergence test and pose
+// update of gicp.py:155-167, on the device so iterations need no host sync.  Run by one wave (lanes
+// 0-63); `sync` orders that wave's LDS traffic.
+template <int D, class Sync>
+__device__ void solve_update(IterState* S, const double* st, Sync sync) {
+    const int lane = threadIdx.x & 63;
     constexpr int NSX = nstat_ext(D);
-    if (lane < NSX) S->stats_solved[lane] = S->stats[lane];
-    if (lane + 64 < NSX) S->stats_solved[lane + 64] = S->stats[lane + 64];
-    const SolveOut<D> r = solve_pose_wave<D>(S->stats, S->T);
-    __syncthreads();   // every lane has read S->T
+    if (lane < NSX) S->stats_solved[lane] = st[lane];
+    if (lane + 64 < NSX) S->stats_solved[lane + 64] = st[lane + 64];
+    const SolveOut<D> r = solve_pose_wave<D>(st, S->T, sync);
+    sync();   // every lane has read S->T
     if (lane != 0) return;
     const int it = S->iter;
     S->iter = it + 1;
     if (!r.ok) S->solve_fail = 1;
     S->loss = r.loss;
     constexpr int NSS = nstat(D);
-    S->pairs_total += S->stats[NSS + 1];
-    const double cnt = S->stats[NSS - 1];
-    const double mse = cnt > 0.0 ? S->stats[NSS + 3] / cnt : 0.0;
+    S->pairs_total += st[NSS + 1];
+    const double cnt = st[NSS - 1];
+    const double mse = cnt > 0.0 ? st[NSS + 3] / cnt : 0.0;
     S->mse = mse;
     if (!S->fixed && fabs(S->last_loss - r.loss) < S->tol) {   // gicp.py:160: stop before the update
         S->converged = 1;
@@ -1916,6 +1916,13 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S) {
         S->converged_at = it;
         S->stop_reason = reason;
     }
+}
+
+// One wave: solve_update on the statistics in the device state (after the multi-GPU all-reduce).
+template <int D>
+__global__ void __launch_bounds__(64) k_solve(IterState* S) {
+    if (S->converged) return;
+    solve_update<D>(S, S->stats, [] { __syncthreads(); });
 }
 
 // ---------------------------------------------------------------------------
