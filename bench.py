@@ -155,6 +155,10 @@ def main():
         t = torch.tensor([elapsed, corr_ms_total], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, corr_ms_total = float(t[0]), float(t[1])
+    if dist is not None:   # every rank releases its communicator, then the process group
+        eng.close()
+        dist.barrier()
+        dist.destroy_process_group()
     if rank != 0:
         return
     from gicp.synthetic import rotation_angle_error, translation_error

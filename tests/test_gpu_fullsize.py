@@ -1,0 +1,125 @@
+"""GPU parity at BASELINE.json's full sizes (configs[1] 100k/100k, configs[2] 1M/1M, configs[4] one
+100k-point LiDAR frame pair): the oracle's cKDTree on the GPU box's host cores checks every
+correspondence of a 1M pass bit-exactly and its statistics to 1e-9, and size-independent properties
+cover the rest (shard additivity, certificates on/off bit-identity, ground-truth recovery)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gicp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+gicp = pytest.importorskip("gicp")
+from gicp import synthetic as S  # noqa: E402
+
+P3 = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+WORKERS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = gicp.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def scene1m():
+    return S.scene_pair_3d(1_000_000)
+
+
+def _pose(deg=1.0, t=(0.06, -0.03, 0.02)):
+    T = np.eye(4)
+    T[:3, :3] = S.axis_angle([0.3, -1.0, 0.7], np.deg2rad(deg))
+    T[:3, 3] = t
+    return T
+
+
+def test_pass_1m_vs_oracle(eng, scene1m):
+    """configs[2]: every one of the 1M correspondence indices equals the oracle's cKDTree answer,
+    W to 1e-9 relative, the 74 statistics to 1e-9 of the oracle's on the same q and W."""
+    src, tgt, _ = scene1m
+    p = gicp.default_params(3, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    C_s = eng.covariances("source")
+    C_t = eng.covariances("target")
+    T = _pose()
+    st, dbg = eng.iterate(T, debug=True)
+    moved = O.apply_transformation(src, T)
+    idx, _ = O.correspondences(moved, tgt, P3["max_distance_correspondence"], workers=WORKERS)
+    assert np.array_equal(dbg["index"], idx)
+    R = T[:3, :3]
+    W = O.weights(np.einsum("ab,nbc,dc->nad", R, C_s, R), C_t, idx)
+    np.testing.assert_allclose(dbg["weight"], W, rtol=1e-9, atol=1e-15)
+    q = np.zeros_like(src)
+    q[idx >= 0] = tgt[idx[idx >= 0]]
+    ref = O.stats(src, q, W, idx, T)
+    np.testing.assert_allclose(st, ref, rtol=1e-9, atol=1e-9 * np.max(np.abs(ref)))
+
+
+def test_covariances_1m_vs_oracle(eng, scene1m):
+    _, tgt, _ = scene1m
+    p = gicp.default_params(3, **P3)
+    eng.set_target(tgt, p)
+    C_gpu = eng.covariances("target")
+    cnt_gpu = eng.neighbor_counts("target")
+    C_or, cnt_or = O.covariances(tgt, P3["max_distance_nearest_neighbors"], workers=WORKERS)
+    assert np.array_equal(cnt_gpu, np.minimum(cnt_or, 20))
+    err = np.max(np.abs(C_gpu - C_or), axis=(1, 2))
+    assert np.quantile(err, 0.999) < 1e-8, np.quantile(err, 0.999)
+    assert np.mean(err > 1e-6) < 1e-3
+
+
+def test_align_1m_properties(eng, scene1m):
+    """30 fixed iterations at 1M (the bench workload): ground truth recovered; 8 shards' statistics
+    sum to the full pass; certificates on/off give bit-identical poses."""
+    src, tgt, Tgt = scene1m
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=30, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    T, res = eng.align(None, p)
+    assert S.rotation_angle_error(T, Tgt) < 2e-5 and S.translation_error(T, Tgt) < 2e-4
+    assert res["iterations"] == 30 and res["correspondences"] > 990_000
+    full = eng.iterate(T)
+    parts = []
+    for s in range(8):
+        eng.set_source(src, p, shard=s, nshards=8)
+        parts.append(eng.iterate(T))
+    np.testing.assert_allclose(np.sum(parts, axis=0), full, rtol=1e-11, atol=1e-11 * np.max(np.abs(full)))
+    os.environ["GICP_NO_CERTS"] = "1"
+    try:
+        e2 = gicp.Engine(0)
+    finally:
+        del os.environ["GICP_NO_CERTS"]
+    try:
+        e2.set_target(tgt, p)
+        e2.set_source(src, p)
+        T2, _ = e2.align(None, p)
+    finally:
+        e2.close()
+    assert np.array_equal(T, T2)
+
+
+def test_align_100k_vs_oracle(eng):
+    """configs[1]: the whole outer loop at 100k/100k against the oracle's (exact inner solves both)."""
+    src, tgt, Tgt = S.scene_pair_3d(100_000)
+    kw = dict(max_iterations=12, tolerance=1e-9, **P3)
+    T, *_ = gicp.gicp(src, tgt, full_output=False, verbose=False, **kw)
+    To, *_ = O.gicp(src, tgt, **kw)
+    assert S.rotation_angle_error(T, To) < 1e-7 and S.translation_error(T, To) < 1e-6
+    assert S.rotation_angle_error(T, Tgt) < 1e-4 and S.translation_error(T, Tgt) < 1e-3
+
+
+def test_lidar_frame_pair_vs_oracle():
+    """configs[4]: one 100k-point spinning-LiDAR frame pair (the odometry step's registration) against
+    the oracle; many source points have no target within d_c here (rejected lanes, certificates of
+    empty neighbourhoods)."""
+    frames = list(S.lidar_stream(3))
+    prev, cur = frames[1][0], frames[2][0]
+    kw = dict(max_iterations=15, tolerance=1e-9, **P3)
+    T, *_ = gicp.gicp(prev, cur, full_output=False, verbose=False, **kw)
+    To, *_ = O.gicp(prev, cur, **kw)
+    assert S.rotation_angle_error(T, To) < 1e-6 and S.translation_error(T, To) < 1e-5
