@@ -262,7 +262,12 @@ float screen_bound(const Margin& m, double d) {
 void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
                       std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out, int k_hint) {
     const int64_t n = (int64_t)codes.size();
-    const int64_t target = (int64_t)(1.35 * std::ceil(n / 64.0)) + 2;
+    static const double budget = [] {   // GICP_TILE_BUDGET: tile-count budget over ceil(n / 64)
+        const char* e = std::getenv("GICP_TILE_BUDGET");
+        const double b = e ? std::atof(e) : 1.35;
+        return b >= 1.0 ? b : 1.35;
+    }();
+    const int64_t target = (int64_t)(budget * std::ceil(n / 64.0)) + 2;
     // decode the grid coordinates once
     auto compact3 = [](uint32_t x) {   // inverse of the kernels' spread3
         x &= 0x09249249u;

@@ -1061,6 +1061,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
         }
         const bool skip_walk = !wave_any(q.valid && !cert);
+        // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
+        // farther than kappa since its last pass (the pose is still converging) walks without it
+        const float kap = cdelta > A.kappa ? 0.f : A.kappa;
 
         // ---- fp32 screen: best and runner-up keys -------------------------
         const unsigned init = __float_as_uint(A.search2) | 63u;
@@ -1072,7 +1075,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (!q.valid || cert) return -1.f;
             const float b = key_d2(best);
             float w = b + 2.f * marg(A.mg, b);
-            const float r = __builtin_amdgcn_sqrtf(b) + A.kappa;
+            const float r = __builtin_amdgcn_sqrtf(b) + kap;
             w = fmaxf(w, r * r);
             return fminf(key_d2(sec), w);
         };
