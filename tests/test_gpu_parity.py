@@ -310,3 +310,39 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     for a, b in zip(out["0"][1], out["1"][1]):
         assert np.array_equal(a, b)
     assert out["0"][3] < 0.05 * out["1"][3]            # the converged pass walked almost nothing
+
+
+def test_large_coordinate_offsets(eng):
+    """Clouds in map coordinates (UTM-like offsets of ~5e6 m): the screen works tile-relative, so the
+    correspondences stay bit-exact and W exact, and the loop still recovers the ground truth."""
+    src, tgt, Tgt = S.scene_pair_3d(20000)
+    off = np.array([451234.5, 5402187.25, 123.0])
+    so, to = src + off, tgt + off
+    p = gicp.default_params(3, **P3)
+    eng.set_target(to, p)
+    eng.set_source(so, p)
+    C_t = eng.covariances("target")
+    C_s = eng.covariances("source")
+    st, dbg = eng.iterate(np.eye(4), debug=True)
+    idx, _ = O.correspondences(so, to, P3["max_distance_correspondence"])
+    assert np.array_equal(dbg["index"], idx)
+    np.testing.assert_allclose(dbg["weight"], O.weights(C_s, C_t, idx), rtol=1e-9, atol=1e-15)
+    p = gicp.default_params(3, max_iterations=40, tolerance=1e-12, **P3)
+    T, _ = eng.align(None, p)
+    Oo = np.eye(4)
+    Oo[:3, 3] = off
+    Tgt_o = Oo @ Tgt @ np.linalg.inv(Oo)          # the same motion expressed in the offset frame
+    # statistics about the far-away origin lose ~8 digits (s s^T ~ 1e13): the pose is judged where it
+    # acts, on the cloud (max point displacement vs the true motion), not by its lever-arm translation
+    disp = np.max(np.linalg.norm(O.apply_transformation(so, T) - O.apply_transformation(so, Tgt_o), axis=1))
+    assert S.rotation_angle_error(T, Tgt_o) < 1e-4 and disp < 5e-3, disp
+
+
+def test_non_finite_input_is_rejected(eng):
+    pts = np.random.default_rng(0).random((100, 3))
+    pts[17, 1] = np.nan
+    with pytest.raises(ValueError):
+        eng.set_target(pts, gicp.default_params(3))
+    pts[17, 1] = np.inf
+    with pytest.raises(ValueError):
+        eng.set_source(pts, gicp.default_params(3))
