@@ -17,6 +17,7 @@
 #include <thread>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -403,21 +404,32 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         tlog += b;
         tprev = t;
     };
-    for (int64_t i = 0; i < n * dim; ++i)
-        if (!std::isfinite(xyz[i])) throw Fail{GICP_E_INVALID, "cloud contains non-finite coordinates"};
     cl.n = 0;   // buffers are kept (grow-only) and reused
     cl.cov_ready = false;
     cl.dim = dim;
     cl.bits = dim == 3 ? 10 : 16;
+    // one fused, branch-free pass: bounds and the finiteness test (v - v is NaN for NaN and +-inf)
     double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-    for (int a = 0; a < dim; ++a) {
-        mn[a] = mx[a] = xyz[a];
-    }
-    for (int64_t i = 0; i < n; ++i)
-        for (int a = 0; a < dim; ++a) {
-            mn[a] = std::min(mn[a], xyz[i * dim + a]);
-            mx[a] = std::max(mx[a], xyz[i * dim + a]);
+    bool finite = true;
+    auto scan = [&](auto D_) {
+        constexpr int D = decltype(D_)::value;
+        double lo[D], hi[D], acc[D];
+        for (int a = 0; a < D; ++a) lo[a] = hi[a] = xyz[a], acc[a] = 0.0;
+        for (int64_t i = 0; i < n; ++i)
+            for (int a = 0; a < D; ++a) {
+                const double v = xyz[i * D + a];
+                lo[a] = v < lo[a] ? v : lo[a];
+                hi[a] = v > hi[a] ? v : hi[a];
+                acc[a] += v - v;
+            }
+        for (int a = 0; a < D; ++a) {
+            mn[a] = lo[a], mx[a] = hi[a];
+            finite = finite && acc[a] == 0.0 && std::isfinite(lo[a]) && std::isfinite(hi[a]);
         }
+    };
+    if (dim == 3) scan(std::integral_constant<int, 3>{});
+    else scan(std::integral_constant<int, 2>{});
+    if (!finite) throw Fail{GICP_E_INVALID, "cloud contains non-finite coordinates"};
     double ext = 0.0;
     for (int a = 0; a < dim; ++a) ext = std::max(ext, mx[a] - mn[a]);
     ext = ext * (1.0 + 1e-9) + 1e-12 * (1.0 + std::fabs(mn[0]));
