@@ -1800,7 +1800,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
             hscale = fmax(hscale, fabs(Hs[k][k]));
         }
         if (gmax == 0.0) break;
-        bool stepped = false;
+        bool stepped = false, flat = false;
         double wmax = 0.0;
         for (int tries = 0; tries < 60; ++tries) {
             double Hd[M][M], ng[M], w[M];
@@ -1810,10 +1810,10 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
                 for (int l = 0; l < M; ++l) Hd[k][l] = Hs[k][l] + (k == l ? lam * (hscale + 1e-300) : 0.0);
                 ng[k] = -grad[k];
             }
+            double dd = 0.0;
             bool ok = chol<M>(Hd);
             if (ok) {
                 chol_solve<M>(Hd, ng, w);
-                double dd = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
                 ok = dd < 0.0;
@@ -1825,6 +1825,12 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
                 wmax = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
+                // the model decrease -dd/2 is below the rounding of f: no step can be resolved, stop
+                // instead of damping towards |w| < 1e-15 (the tries would only chase rounding noise)
+                if (fn > f && -dd <= kFlatEps * fabs(f)) {
+                    flat = true;
+                    break;
+                }
                 if (fn <= f || wmax < 1e-15) {
                     if (fn <= f) {
 #pragma unroll
@@ -1840,7 +1846,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
             }
             lam = lam == 0.0 ? 1e-9 : lam * 10.0;
         }
-        if (!stepped || wmax < 1e-15) break;
+        if (!stepped || flat || wmax < 1e-15) break;
     }
 #pragma unroll
     for (int a = 0; a < D; ++a) {

@@ -15,6 +15,17 @@
 namespace gicp {
 
 #define GICP_HD __host__ __device__ __forceinline__
+// probes for solver experiments (a host harness defines them; no-ops in the library)
+#ifndef GICP_SOLVER_PROBE_ITER
+#define GICP_SOLVER_PROBE_ITER() ((void)0)
+#define GICP_SOLVER_PROBE_TRY() ((void)0)
+#endif
+
+// Newton stops when a rejected step's model decrease -dd/2 is within 4 ulps of the loss
+#ifndef GICP_FLAT_EPS
+#define GICP_FLAT_EPS 8.0
+#endif
+constexpr double kFlatEps = GICP_FLAT_EPS * 2.220446049250313e-16;
 
 template <int D>
 struct SolveOut {
@@ -237,6 +248,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
     double f = phi(R);
     double lam = 0.0;
     for (int it = 0; it < 100; ++it) {
+        GICP_SOLVER_PROBE_ITER();
         double u[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -286,9 +298,10 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
             hscale = fmax(hscale, fabs(Hs[k][k]));
         }
         if (gmax == 0.0) break;
-        bool stepped = false;
+        bool stepped = false, flat = false;
         double wmax = 0.0;
         for (int tries = 0; tries < 60; ++tries) {
+            GICP_SOLVER_PROBE_TRY();
             double Hd[M][M], ng[M], w[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) {
@@ -296,10 +309,10 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
                 for (int l = 0; l < M; ++l) Hd[k][l] = Hs[k][l] + (k == l ? lam * (hscale + 1e-300) : 0.0);
                 ng[k] = -grad[k];
             }
+            double dd = 0.0;
             bool ok = chol<M>(Hd);
             if (ok) {
                 chol_solve<M>(Hd, ng, w);
-                double dd = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
                 ok = dd < 0.0;
@@ -311,6 +324,12 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
                 wmax = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
+                // the model decrease -dd/2 is below the rounding of f: no step can be resolved, stop
+                // instead of damping towards |w| < 1e-15 (the tries would only chase rounding noise)
+                if (fn > f && -dd <= kFlatEps * fabs(f)) {
+                    flat = true;
+                    break;
+                }
                 if (fn <= f || wmax < 1e-15) {
                     if (fn <= f) {
 #pragma unroll
@@ -325,7 +344,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
             }
             lam = lam == 0.0 ? 1e-9 : lam * 10.0;
         }
-        if (!stepped || wmax < 1e-15) break;
+        if (!stepped || flat || wmax < 1e-15) break;
     }
     // t from the eliminated block
 #pragma unroll
