@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--shard-sim", type=int, default=1,
                     help="diagnostic: one process runs only shard 0 of S (no collective) to time a rank of an "
                          "S-GPU job; the line is marked and is not the metric")
+    ap.add_argument("--shard-index", type=int, default=0, help="diagnostic: which shard --shard-sim runs")
     return ap.parse_args()
 
 
@@ -118,7 +119,7 @@ def main():
     t0 = time.perf_counter()
     eng.set_target(tgt, params)
     if world == 1 and a.shard_sim > 1:
-        eng.set_source(src, params, shard=0, nshards=a.shard_sim)
+        eng.set_source(src, params, shard=a.shard_index, nshards=a.shard_sim)
     else:
         eng.set_source(src, params, shard=rank, nshards=world)
     setup_ms = (time.perf_counter() - t0) * 1e3
@@ -199,7 +200,7 @@ def main():
         "ambiguous_last_pass": res["ambiguous"],
     }
     if a.shard_sim > 1 and world == 1:
-        line["diagnostic"] = f"shard 0 of {a.shard_sim} only, no all-reduce: one rank of a {a.shard_sim}-GPU job"
+        line["diagnostic"] = f"shard {a.shard_index} of {a.shard_sim} only, no all-reduce: one rank of a {a.shard_sim}-GPU job"
         line["cpu_baseline"] = None
         print(json.dumps(line))
         return

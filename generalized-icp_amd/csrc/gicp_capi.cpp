@@ -35,7 +35,7 @@ hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, int64_t, int, double*, int32_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
-int corr_grid(int, int);
+int corr_grid(int q_tiles, int shard, int nshards);
 int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
 }  // namespace gicp
 
@@ -387,9 +387,9 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
     cut(E, true);
 }
 
-// Build the device index of a cloud and its per-point covariances for tiles [qb, qe) (qe < 0: all).
-void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, int shard,
-                 int nshards, bool cov_all) {
+// Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
+// is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
+void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -489,12 +489,8 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         std::memcpy(&cl.rho, &rho_bits, sizeof(float));
         tick("tiles");
 
-        // surface covariances (gicp.py:19-35) for this rank's query tiles
-        int qb = 0, qe = cl.ntiles;
-        if (!cov_all) {
-            qb = (int)((int64_t)cl.ntiles * shard / nshards);
-            qe = (int)((int64_t)cl.ntiles * (shard + 1) / nshards);
-        }
+        // surface covariances (gicp.py:19-35)
+        const int qb = 0, qe = cl.ntiles;
         CovArgs ca{};
         ca.cl = cl.view();
         ca.q_begin = qb;
@@ -541,8 +537,8 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
     c->shard = shard;
     c->nshards = nshards;
-    c->q_begin = (int)((int64_t)c->src.ntiles * shard / nshards);
-    c->q_end = (int)((int64_t)c->src.ntiles * (shard + 1) / nshards);
+    c->q_begin = 0;   // k_corr maps this rank's units onto the cloud's (interleaved chunks)
+    c->q_end = c->src.ntiles;
     const int nt = std::max(1, c->src.ntiles);
     dreserve(c->d_hint, c->cap_hint, nt);
     dreserve(c->d_list, c->cap_list, (size_t)nt * kListMax);
@@ -553,7 +549,7 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     dreserve(c->d_cert_j, c->cap_cj, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_gap, c->cap_cg, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_pass, c->cap_cp, nt);
-    const int q8 = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim) / 8);
+    const int q8 = std::max(1, corr_grid(c->src.ntiles, c->shard, c->nshards) / 8);
     dreserve(c->d_order, c->cap_order, (size_t)2 * 8 * kOrderBuckets * q8);
     if (!c->d_order_cnt) dalloc(c->d_order_cnt, 2 * 8 * kOrderBuckets);
     reset_tile_state(c);
@@ -561,7 +557,7 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
 
 void ensure_workspace(gicp_ctx* c) {
     const int nsx = nstat_ext(3);
-    const int grid = std::max(1, corr_grid(c->q_end - c->q_begin, c->src.dim));
+    const int grid = std::max(1, corr_grid(c->src.ntiles, c->shard, c->nshards));
     if ((grid + kGroupWG - 1) / kGroupWG > kMaxGroups) throw Fail{GICP_E_INVALID, "source shard too large"};
     const size_t need = (size_t)grid * nsx;
     if (need > c->partials_cap) {
@@ -586,6 +582,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.tgt = c->tgt.view();
     a.q_begin = c->q_begin;
     a.q_end = c->q_end;
+    a.sh_skip = (c->nshards - 1) * kShardChunk;
+    a.sh_first = c->shard * kShardChunk;
     a.state = c->d_state;
     a.tickets = c->d_tickets;
     a.gpart = c->d_gpart;
@@ -717,7 +715,7 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
         }
     }
     const int nsx = nstat_ext(d);
-    const int grid = corr_grid(c->q_end - c->q_begin, d);
+    const int grid = corr_grid(c->src.ntiles, c->shard, c->nshards);
 #if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
     static unsigned long long* d_stamps = nullptr;
     static size_t stamps_cap = 0;
@@ -906,7 +904,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, 0, 1, true);
+        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt);
         if (c->src.n) reset_tile_state(c);
     });
 }
@@ -918,7 +916,7 @@ int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gi
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         c->psrc = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c, c->src, xyz, N, dim, c->psrc, shard, nshards, nshards == 1);
+        build_cloud(c, c->src, xyz, N, dim, c->psrc);
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
     });
@@ -1051,7 +1049,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         hs.pairs_total = 0.0;
         hs.converged_at = -1;
         HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
-        const int grid = corr_grid(c->q_end - c->q_begin, d);
+        const int grid = corr_grid(c->src.ntiles, c->shard, c->nshards);
         const bool timing = res != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         double corr_ms = 0.0;

@@ -109,11 +109,20 @@ struct IterState {
 };
 
 constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
+// Source shards are interleaved in chunks of kShardChunk units (a unit = kCorrWaves source tiles,
+// one k_corr workgroup): rank r of G reduces global chunks r, r + G, r + 2G, ...  Contiguous Morton
+// ranges left the ranks unbalanced (the registration's far walls are the heavy tiles: one rank of 8
+// took 1.7x another's k_corr time), and every rank waits for the slowest at the all-reduce.  A chunk
+// of 64 tiles is still one compact region, so an XCD's L2 keeps its locality.
+constexpr int kShardChunk = 16;
 constexpr int kMaxGroups = 4096;   // ticket counters available
 
 struct CorrArgs {
     DevCloud src, tgt;
-    int32_t q_begin, q_end;   // this rank's source tiles
+    int32_t q_begin, q_end;   // k_corr: q_begin unused (0), q_end = the cloud's tile count
+    // source shards (interleaved by kShardChunk units): this rank's unit u is the cloud's unit
+    // u + (u / kShardChunk) sh_skip + sh_first, sh_skip = (G - 1) kShardChunk, sh_first = r kShardChunk
+    int32_t sh_skip, sh_first;
     IterState* state;         // pose in, statistics out
     uint32_t* tickets;        // [kMaxGroups + 1] arrival counters, zero between launches (self-resetting)
     double* gpart;            // [kMaxGroups][nstat_ext] group partials

@@ -982,7 +982,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     }
     unit = __builtin_amdgcn_readfirstlane(unit);
     const unsigned long long wg_t0 = __builtin_amdgcn_s_memtime();
-    int T = A.q_begin + unit * kCorrWaves + w;
+    // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
+    int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;
     if (T >= A.q_end) T = -1;
     if (T >= 0) {
     bool on = false;          // accepted correspondence
@@ -2097,10 +2098,16 @@ hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Workgroups (units) of a k_corr launch: kCorrWaves source tiles each.
-int corr_grid(int q_tiles, int /*dim*/) {
+// Workgroups (units) of a k_corr launch: kCorrWaves source tiles each; with shards, the units of
+// the global chunks shard, shard + nshards, ... (kShardChunk units each, the last one possibly partial).
+int corr_grid(int q_tiles, int shard, int nshards) {
     if (q_tiles <= 0) return 0;
-    return (q_tiles + kCorrWaves - 1) / kCorrWaves;
+    const int units = (q_tiles + kCorrWaves - 1) / kCorrWaves;
+    if (nshards <= 1) return units;
+    const int nchunks = (units + kShardChunk - 1) / kShardChunk;
+    int mine = 0;
+    for (int c = shard; c < nchunks; c += nshards) mine += std::min(kShardChunk, units - c * kShardChunk);
+    return mine;
 }
 
 hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {

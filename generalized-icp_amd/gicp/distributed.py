@@ -4,7 +4,8 @@ The reference has no parallelism (its only concurrency is a pygame worker
 process, robot-visualization.py:151-166,199).  Here the per-iteration work
 partitions naturally: every rank holds the whole target (index + covariances)
 and the whole source (its covariance neighbourhoods need all points), and
-reduces only its shard of Morton-contiguous source tiles.  The one exchange
+reduces only its shard of source tiles: chunks of 64 Morton-consecutive tiles
+dealt round-robin over the ranks (``shard_tiles``).  The one exchange
 per iteration is an all-reduce (sum) of the 74 fp64 statistics (26 in 2-D);
 every rank then runs the identical host solve and the identical convergence
 test, so no pose broadcast is needed.  Inside libgicp_hip.so that all-reduce
@@ -30,9 +31,18 @@ def init_comm(engine: Engine, rank: int, world: int, group=None):
     engine.comm_init(world, rank, uid[0])
 
 
+UNIT_TILES = 4      # source tiles per k_corr workgroup (kCorrWaves)
+SHARD_CHUNK = 16    # units per shard chunk (kShardChunk, csrc/gicp_internal.h)
+
+
 def shard_tiles(ntiles: int, rank: int, world: int):
-    """Tile range [begin, end) reduced by `rank` (the split gicp_set_source applies)."""
-    return ntiles * rank // world, ntiles * (rank + 1) // world
+    """Source tiles reduced by `rank` (the split gicp_set_source applies): the cloud's units of
+    UNIT_TILES tiles are cut into chunks of SHARD_CHUNK units and rank r takes chunks r, r + world, ...
+    (interleaved, so the heavy regions of a registration spread over the ranks)."""
+    per = UNIT_TILES * SHARD_CHUNK
+    nchunks = -(-ntiles // per)
+    return np.concatenate([np.arange(c * per, min(ntiles, (c + 1) * per), dtype=np.int64)
+                           for c in range(rank, nchunks, world)] or [np.zeros(0, np.int64)])
 
 
 def align(engine: Engine, source, target, params, rank: int, world: int, T0=None):
