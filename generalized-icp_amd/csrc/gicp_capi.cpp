@@ -530,6 +530,8 @@ void reset_tile_state(gicp_ctx* c) {
     HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
     HIPCHK(hipMemsetAsync(c->d_order_cnt, 0, sizeof(int32_t) * 2 * 8 * kOrderBuckets, c->stream));
     if (c->d_cert_pass) HIPCHK(hipMemsetAsync(c->d_cert_pass, 0xFF, sizeof(int32_t) * nt, c->stream));
+    // last matches (k_corr's per-lane search cap): none yet
+    if (c->d_cert_j) HIPCHK(hipMemsetAsync(c->d_cert_j, 0xFF, sizeof(int32_t) * std::max<int64_t>(1, c->src.n), c->stream));
     c->pass = 0;
 }
 

@@ -1070,15 +1070,37 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         const unsigned init = __float_as_uint(A.search2) | 63u;
         unsigned best = init, sec = init;
         int best_tile = -1;
-        // lane search bound: the runner-up, or the winner plus the screen's ambiguity band, widened to
-        // (sqrt(b) + kappa)^2 when certificates are kept so the runner-up gap is known up to kappa
+        // the bound as a function of the winner's screened d2 b: the winner plus the screen's ambiguity
+        // band, widened to (sqrt(b) + kappa)^2 when certificates are kept (runner-up gap known up to kappa)
+        auto bound_of = [&](float b) -> float {
+            const float w = b + 2.f * marg(A.mg, b);
+            const float r = __builtin_amdgcn_sqrtf(b) + kap;
+            return fmaxf(w, r * r);
+        };
+        // Search cap from the last pass's match jp of this point (any target bounds the nearest's
+        // distance): d2 to jp estimated in fp32 (error within the screen margin, like the screen's own),
+        // so the screened winner's d2 is <= b0 = d2 + 2 margin and the bound the walk would end with is
+        // <= bound_of(b0).  Lanes start the walk at that radius instead of the screen radius; every row
+        // within the final bound is still scanned, so the result is unchanged (bit-identical, tested).
+        float cap = 3e38f;
+        if (A.cert_j && q.valid && !cert && !skip_walk) {
+            const int jp = A.cert_j[i];
+            if (jp >= 0 && jp < tg.n) {
+                const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[jp];
+                const double tv[3] = {t4.x, t4.y, t4.z};
+                float d2 = 0.f;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const float d = (float)(q.ow[a] - tv[a]) + q.pw[a];
+                    d2 = fmaf(d, d, d2);
+                }
+                cap = bound_of(d2 + 2.f * marg(A.mg, d2)) * 1.0001f;
+            }
+        }
+        // lane search bound: the runner-up, or bound_of(winner), within the cap
         auto lane_bound = [&]() -> float {
             if (!q.valid || cert) return -1.f;
-            const float b = key_d2(best);
-            float w = b + 2.f * marg(A.mg, b);
-            const float r = __builtin_amdgcn_sqrtf(b) + kap;
-            w = fmaxf(w, r * r);
-            return fminf(key_d2(sec), w);
+            return fminf(cap, fminf(key_d2(sec), bound_of(key_d2(best))));
         };
         float lb = lane_bound();   // refreshed after every merge
         // lb inflated by the rounding slack, for the slack-free box tests
