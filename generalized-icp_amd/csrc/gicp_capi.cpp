@@ -110,7 +110,7 @@ struct Cloud {
     }
     void reserve_tiles(int nt, int nb) {
         dreserve(tiles, cap_tiles, (size_t)nt);
-        dreserve(blocks, cap_blocks, (size_t)nb);
+        dreserve(blocks, cap_blocks, (size_t)nb + (nb + kBlockTiles - 1) / kBlockTiles);   // + super-blocks
         dreserve(tile_code, cap_tcode, (size_t)nt);
     }
     void release() {
@@ -201,6 +201,7 @@ struct gicp_ctx {
     bool use_lists = true;
     bool use_order = true;            // GICP_NO_ORDER=1: identity workgroup order
     double skin_frac = 0.2;           // candidate-list skin as a fraction of d_c (GICP_SKIN)
+    double skin_gain = 1.0;           // adaptive skin: multiple of the tile's last displacement (GICP_SKIN_GAIN)
     double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -616,6 +617,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.pass = ++c->pass;
     a.use_lists = c->use_lists ? 1 : 0;
     a.skin = (float)(c->skin_frac * dc);
+    a.skin_gain = (float)c->skin_gain;
+    a.skin_max = (float)dc;
     a.gap_slack = (float)std::ldexp(std::sqrt((double)a.search2) + 2.0 * c->tgt.rho + 2.0 * c->src.rho, -19);
     a.cov_model = c->psrc.cov_model;
     a.pl_inv = 1.0 / (c->ptgt.epsilon * (1.0 - c->ptgt.ratio));   // target m = sqrt(eps (1 - ratio)) n
@@ -805,6 +808,7 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_NO_ORDER")) c->use_order = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
+    if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;

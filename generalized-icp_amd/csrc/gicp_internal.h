@@ -53,7 +53,7 @@ struct DevCloud {
     const double4* cov;       // [n]     (a, m0, m1, m2): C = a I - m m^T
     const int32_t* perm;      // [n]     sorted -> original index
     const TileInfo* tiles;    // [ntiles]
-    const BlockInfo* blocks;  // [nblocks]
+    const BlockInfo* blocks;  // [nblocks] blocks of 64 tiles, then [ceil(nblocks / 64)] super-blocks of 64 blocks
     const uint32_t* tile_code;// [ntiles] Morton code of each tile's first point
     int64_t n;
     int32_t ntiles;
@@ -151,6 +151,9 @@ struct CorrArgs {
     int32_t pass;             // this pass's id (monotonic per source cloud)
     int32_t use_lists;        // 0: always full walk (no lists)
     float skin;
+    // a tile rebuilding its list while the pose still moves uses skin' = min(max(skin, skin_gain x its
+    // displacement over the last pass), skin_max): the list then outlasts a step of the same size
+    float skin_gain, skin_max;
     // per-source-point nearest-neighbour certificates, sorted source order; null: off
     int32_t* cert_j;          // [src.n] sorted target index of the certified nearest, -1: none within R
     float* cert_gap;          // [src.n] runner-up gap (found) or empty radius R (none), relative to cert_pass

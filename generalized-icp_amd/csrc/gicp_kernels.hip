@@ -11,7 +11,7 @@
 //   k_solve     <- the inner solve + convergence test on the device (gicp.py:148-167)
 //
 // Design: one wave = one query tile of <= 64 Morton-coherent points.
-// Database tiles are culled with a two-level AABB hierarchy (blocks of 64 tiles, tested
+// Database tiles are culled with a three-level AABB hierarchy (super-blocks of 64 blocks of 64 tiles, tested
 // one per lane, ballot), staged through LDS as fp32 SoA and scanned with a
 // broadcast read; lanes keep packed (d2 | row) keys.  The fp32 screen carries an
 // explicit error bound: a lane whose winner is within that bound of a rival (or of
@@ -250,17 +250,20 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
 }
 
 // One wave per block of 64 tiles: fp64 AABB over the tiles' boxes.
-__global__ void __launch_bounds__(256) k_build_blocks(const TileInfo* __restrict__ tiles, int ntiles, BlockInfo* blocks,
+// One level of the box hierarchy: box B covers children [64 B, 64 B + 64) of the level below
+// (tiles -> blocks; blocks -> super-blocks, stored after the blocks in the same array).
+template <class Child>
+__global__ void __launch_bounds__(256) k_build_blocks(const Child* __restrict__ kids, int nkids, BlockInfo* blocks,
                                                        int nblocks, int dim) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int B = blockIdx.x * kWavesPerWG + w;
     if (B >= nblocks) return;
     const int t = B * kBlockTiles + l;
-    const bool v = t < ntiles;
+    const bool v = t < nkids;
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-        lo[a] = v ? tiles[t].c[a] - (double)tiles[t].h[a] : 1e300;
-        hi[a] = v ? tiles[t].c[a] + (double)tiles[t].h[a] : -1e300;
+        lo[a] = v ? kids[t].c[a] - (double)kids[t].h[a] : 1e300;
+        hi[a] = v ? kids[t].c[a] + (double)kids[t].h[a] : -1e300;
         lo[a] = wave_mind(lo[a]);
         hi[a] = wave_maxd(hi[a]);
     }
@@ -273,7 +276,7 @@ __global__ void __launch_bounds__(256) k_build_blocks(const TileInfo* __restrict
             b.h[a] = __double2float_ru(hh) * (1.0f + 1e-6f);
         }
         b.first = B * kBlockTiles;
-        b.ntiles = min(kBlockTiles, ntiles - B * kBlockTiles);
+        b.ntiles = min(kBlockTiles, nkids - B * kBlockTiles);
         b.pad = 0.f;
     }
 }
@@ -332,7 +335,18 @@ __device__ __forceinline__ void traverse_c(const DevCloud& db, const Query<D>& q
             wbi = infl(wb);
         }
     }
+    // super-blocks (64 blocks each, stored after the blocks): a round of 64 block tests is one
+    // super-block, skipped whole when its box (scalar loads, uniform test) is out of reach.  It contains
+    // its blocks' boxes, so the visited tiles and their order are unchanged.
+    typedef __attribute__((address_space(4))) const BlockInfo* ConstBlocks;
+    const ConstBlocks cb0 = (ConstBlocks)(uintptr_t)db.blocks + db.nblocks;
     for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
+        {
+            const ConstBlocks sb = cb0 + (b0 / kWave);
+            const double c[3] = {sb->c[0], sb->c[1], sb->c[2]};
+            const float h[3] = {sb->h[0], sb->h[1], sb->h[2]};
+            if (!__builtin_amdgcn_readfirstlane((int)(gap2_box<D>(q, c, h) <= wbi))) continue;   // uniform
+        }
         if (cnt) cnt->count(5);
         const int b = b0 + l;
         bool cb = false;
@@ -1211,17 +1225,22 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
         }
         if (!use && !skip_walk) {
+            float skin = A.skin;   // adaptive: a moving tile's list covers a step like its last one
+            if (lists && A.skin_gain > 0.f) {
+                const float dl = disp_since(A.pass - 1);
+                if (dl > 0.f) skin = fminf(fmaxf(skin, A.skin_gain * dl), A.skin_max);
+            }
             int ncol = 0;
             int cent = 0x7fffffff;   // lane k: collected entry k
             auto collect = [&](int Tt) {
                 if (l == ncol) cent = Tt;
                 ++ncol;
             };
-            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, lists ? A.skin : 0.f,
+            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, lists ? skin : 0.f,
                           collect, &S);
             if (lists) {
                 const float wbf = wave_maxf(lb);
-                const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + A.skin : 0.f;
+                const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + skin : 0.f;
                 if (ncol <= kListMax) {   // store nearest-first: by centre distance to the wave box
                     float key = 3e38f;
                     if (l < ncol) {
@@ -2104,7 +2123,11 @@ hipError_t launch_build_tiles(const double* xyz_in, int dim, const int32_t* perm
 hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blocks, int nblocks, int dim,
                                hipStream_t st) {
     const unsigned g = (unsigned)((nblocks + kWavesPerWG - 1) / kWavesPerWG);
-    hipLaunchKernelGGL(k_build_blocks, dim3(g), dim3(256), 0, st, tiles, ntiles, blocks, nblocks, dim);
+    hipLaunchKernelGGL(k_build_blocks<TileInfo>, dim3(g), dim3(256), 0, st, tiles, ntiles, blocks, nblocks, dim);
+    const int nsuper = (nblocks + kBlockTiles - 1) / kBlockTiles;   // super-blocks at blocks[nblocks..]
+    const unsigned g2 = (unsigned)((nsuper + kWavesPerWG - 1) / kWavesPerWG);
+    hipLaunchKernelGGL(k_build_blocks<BlockInfo>, dim3(g2), dim3(256), 0, st, (const BlockInfo*)blocks, nblocks,
+                       blocks + nblocks, nsuper, dim);
     return hipGetLastError();
 }
 
