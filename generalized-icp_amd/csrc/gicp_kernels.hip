@@ -1067,11 +1067,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         bool cert = false;
         int cj = -1;
         float cgap = 0.f, cdelta = -1.f;
+        int jp = -1;   // the point's last match (loaded unconditionally: in flight with cert_pass)
         if (A.cert_j) {
+            jp = A.cert_j[i];
+            const float g0 = A.cert_gap[i];
             cdelta = disp_since(A.cert_pass[T]);
             if (cdelta >= 0.f && q.valid) {
-                cj = A.cert_j[i];
-                cgap = A.cert_gap[i];
+                cj = jp;
+                cgap = g0;
                 cert = cj >= 0 ? 2.f * cdelta < cgap : cgap - cdelta > A.empty_r;
             }
         }
@@ -1098,7 +1101,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // within the final bound is still scanned, so the result is unchanged (bit-identical, tested).
         float cap = 3e38f;
         if (A.cert_j && q.valid && !cert && !skip_walk) {
-            const int jp = A.cert_j[i];
             if (jp >= 0 && jp < tg.n) {
                 const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[jp];
                 const double tv[3] = {t4.x, t4.y, t4.z};
@@ -1376,14 +1378,16 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         S.mark(4);
         // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
         if (found && j >= 0) {
+            // match position and both covariances requested together (one memory round trip)
             const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
+            const double4 ct = tg.cov[j];
+            const double4 cs = sc.cov[i];
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
             const double dist = sqrt(d2e);
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = dist;
             if (!(dist > A.dc)) {  // gicp.py:136: reject only if distance > d_c
                 on = true;
-                const double4 ct = tg.cov[j];
                 const double mt[3] = {ct.y, ct.z, ct.w};
                 if (A.cov_model == GICP_COV_POINT_TO_POINT) {          // C_s = 0, C_t = I: W = I
 #pragma unroll
@@ -1396,7 +1400,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #pragma unroll
                         for (int b = 0; b < D; ++b) W[a][b] = mt[a] * mt[b] * A.pl_inv;
                 } else {
-                const double4 cs = sc.cov[i];
                 const double ms[3] = {cs.y, cs.z, cs.w};
                 double mr[D];
 #pragma unroll
