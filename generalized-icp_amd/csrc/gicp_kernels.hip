@@ -1288,7 +1288,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             amb = (s2 - b) <= marg(A.mg, b) + marg(A.mg, s2);
             j = tg.tiles[best_tile].start + (int)(best & 63u);
         }
-        if (A.cert_j) {   // every lane's certificate is restated relative to this pass's pose
+        // Every lane's certificate is restated relative to this pass's pose where the wave walked; a wave
+        // that skipped the walk leaves its certificates (and cert_pass) as they are: they stay relative to
+        // the older pose, whose direct displacement to later poses is no larger than the summed steps,
+        // and the pass writes nothing for it -- until that pose is half the pose ring old.
+        if (A.cert_j && (!skip_walk || A.pass - A.cert_pass[T] >= kPoseRing / 2)) {
             if (q.valid) {
                 float g = 0.f;
                 if (cert) {

@@ -32,6 +32,6 @@ print("== steady state (after %d iterations)" % a.iters, file=sys.stderr, flush=
 eng.iterate(T)
 eng.iterate(T)
 print("== early (after 2 iterations from identity, fresh lists)", file=sys.stderr, flush=True)
-p.max_iterations = 2
+p.max_iterations = int(os.environ.get("EARLY_ITERS", "2"))
 T2, _ = eng.align(None, p)
 eng.iterate(T2)
