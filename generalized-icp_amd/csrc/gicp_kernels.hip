@@ -879,19 +879,19 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 // ---------------------------------------------------------------------------
 // Register budget of k_corr: on gfx950 a wave with next_free_sgpr >= 94 leaves 6 waves per SIMD,
 // <= 90 leaves 7 and <= 72 (with <= 64 VGPRs) 8 (scripts/probes/occupancy.hip measures it; the
-// compiler's own occupancy estimate does not model it).
+// compiler's own occupancy estimate does not model it).  6 waves per SIMD: 75 VGPRs, no VGPR spill;
+// held to 7 (72 VGPRs, 88 SGPRs) the allocator spills 6 VGPRs and ~30 SGPRs, and the 1M/1M bench ran
+// 0.7-1.3 % slower (interleaved A/B, scripts/variants.sh) once the per-lane search cap and the adaptive
+// list skin were in (it was the faster setting before them).
 #ifndef GICP_CORR_ATTR
 #if defined(GICP_CORR_WAVES_PER_EU)
 #define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(GICP_CORR_WAVES_PER_EU, GICP_CORR_WAVES_PER_EU)))
-#elif defined(GICP_TIMELINE)   // keep the diagnostic build at the product's 7 waves per SIMD
-#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(7, 7)))
-#else   // 7 waves per SIMD: at 73 VGPRs the allocator would settle for 6; held to 72 it spills one
-        // double once per wave (stored in the prologue, reloaded for the statistics)
-#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(7, 7)))
+#else
+#define GICP_CORR_ATTR __attribute__((amdgpu_num_sgpr(GICP_CORR_SGPR), amdgpu_waves_per_eu(6, 6)))
 #endif
 #endif
 #ifndef GICP_CORR_SGPR
-#define GICP_CORR_SGPR 88
+#define GICP_CORR_SGPR 100
 #endif
 
 template <int D>
