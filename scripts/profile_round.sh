@@ -5,7 +5,6 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
-timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o t --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/trace.err || { echo trace failed; exit 1; }
 python3 scripts/trace_iters.py $OUT/trace 30 > $OUT/iterations.txt
 i=0
@@ -18,4 +17,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_I
 done
 python3 scripts/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt
 python3 scripts/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json k_corr 3d_room_1000k_1000k_k20
+# the bench line last: its roofline.traffic reads the pmc_traffic.json written above (copied to profiles/)
+cp $OUT/pmc_traffic.json profiles/r01/pmc_traffic.json
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
 echo done
