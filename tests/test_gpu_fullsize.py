@@ -89,18 +89,21 @@ def test_align_1m_properties(eng, scene1m):
         eng.set_source(src, p, shard=s, nshards=8)
         parts.append(eng.iterate(T))
     np.testing.assert_allclose(np.sum(parts, axis=0), full, rtol=1e-11, atol=1e-11 * np.max(np.abs(full)))
-    os.environ["GICP_NO_CERTS"] = "1"
-    try:
-        e2 = gicp.Engine(0)
-    finally:
-        del os.environ["GICP_NO_CERTS"]
-    try:
-        e2.set_target(tgt, p)
-        e2.set_source(src, p)
-        T2, _ = e2.align(None, p)
-    finally:
-        e2.close()
-    assert np.array_equal(T, T2)
+    # without certificates (and their search cap), then also without candidate lists: same poses, bit for bit
+    for env in ({"GICP_NO_CERTS": "1"}, {"GICP_NO_CERTS": "1", "GICP_NO_LISTS": "1"}):
+        os.environ.update(env)
+        try:
+            e2 = gicp.Engine(0)
+        finally:
+            for k in env:
+                del os.environ[k]
+        try:
+            e2.set_target(tgt, p)
+            e2.set_source(src, p)
+            T2, _ = e2.align(None, p)
+        finally:
+            e2.close()
+        assert np.array_equal(T, T2), env
 
 
 def test_align_100k_vs_oracle(eng):

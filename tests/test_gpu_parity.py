@@ -282,15 +282,18 @@ def test_one_rank_rccl_allreduce_is_identity(scene3d):
 
 
 def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
-    """Per-point nearest-neighbour certificates skip the walk for lanes whose nearest
-    target is provably unchanged: a 60-iteration fixed run and single passes around its endpoint must
-    be bit-identical to an engine without them (GICP_NO_CERTS=1), while the certified passes evaluate
-    far fewer pairs."""
+    """Per-point nearest-neighbour certificates and the per-lane search cap from the last match
+     skip or shorten walks for lanes whose nearest target is provably unchanged; the
+    candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
+    A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
+    default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
+    certificates or lists (plain full walks), while the certified passes evaluate far fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1"):
-        monkeypatch.setenv("GICP_NO_CERTS", flag)
+    for flag in ("0", "1", "plain"):
+        monkeypatch.setenv("GICP_NO_CERTS", "0" if flag == "0" else "1")
+        monkeypatch.setenv("GICP_NO_LISTS", "1" if flag == "plain" else "0")
         e = gicp.Engine(0)
         try:
             e.set_target(tgt, p)
@@ -306,9 +309,10 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    assert np.array_equal(out["0"][0], out["1"][0])
-    for a, b in zip(out["0"][1], out["1"][1]):
-        assert np.array_equal(a, b)
+    for other in ("1", "plain"):
+        assert np.array_equal(out["0"][0], out[other][0])
+        for a, b in zip(out["0"][1], out[other][1]):
+            assert np.array_equal(a, b)
     assert out["0"][3] < 0.05 * out["1"][3]            # the converged pass walked almost nothing
 
 
