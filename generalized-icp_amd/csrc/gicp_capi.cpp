@@ -27,7 +27,7 @@
 
 namespace gicp {
 hipError_t launch_morton(const double*, int64_t, int, const DevCloud&, uint32_t*, int32_t*, hipStream_t);
-hipError_t launch_build_tiles(const double*, int, const int32_t*, TileInfo*, int, double*, float4*, int32_t*,
+hipError_t launch_build_tiles(const double*, int, int32_t*, TileInfo*, int, double*, float4*, int32_t*,
                               unsigned*, hipStream_t);
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);

@@ -182,8 +182,55 @@ __global__ void k_morton(const double* __restrict__ xyz, int64_t n, int dim, Dev
 
 // One wave per tile: gather the tile's points (original order -> sorted), fp64 AABB,
 // centre, fp32 relative coordinates, half-extents and radius.
+// Order of the rows inside a tile: a two-level median split instead of the Morton order the tile
+// was cut from.  Rows 0-31 / 32-63 are the halves along the tile's longest axis, and each half is
+// ordered along its own longest axis, so the four 16-row sub-tiles are compact boxes (a Morton run
+// of 16 can straddle a cell boundary and span the whole tile).  Rows carry no meaning beyond the
+// sub-tile boxes (ties are resolved on original indices), so only the culling changes.
+__device__ __forceinline__ void split_order(double (&p)[3], int& o, int dim, bool v) {
+    const int l = lane_id();
+    auto longest = [&](const double* mn, const double* mx) {
+        int ax = 0;
+        for (int a = 1; a < dim; ++a)
+            if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
+        return ax;
+    };
+    auto gather = [&](int src) {
+        for (int a = 0; a < 3; ++a) p[a] = __shfl(p[a], src);
+        o = __shfl(o, src);
+    };
+    double mn[3], mx[3];
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = wave_mind(v ? p[a] : 1e300);
+        mx[a] = wave_maxd(v ? p[a] : -1e300);
+    }
+    const int ax = longest(mn, mx);
+    float key = v ? (float)(p[ax] - mn[ax]) : 3e38f;   // invalid rows sort last
+    int src = l;
+    wave_sort64(key, src);
+    gather(src);
+    // second level: each 32-row half along its own longest axis (xor offsets < 32 stay in the half)
+    const int cnt = __popcll(__ballot(v));
+    const bool vv = l < cnt;
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = vv ? p[a] : 1e300;
+        mx[a] = vv ? p[a] : -1e300;
+        for (int s = 1; s < 32; s <<= 1) {
+            mn[a] = fmin(mn[a], __shfl_xor(mn[a], s));
+            mx[a] = fmax(mx[a], __shfl_xor(mx[a], s));
+        }
+    }
+    const int ax2 = longest(mn, mx);
+    const double span = mx[ax2] - mn[ax2];
+    const float t = span > 0.0 ? (float)((p[ax2] - mn[ax2]) / span) : 0.f;
+    key = vv ? (float)(2 * (l >> 5)) + t : 3e38f;   // half 0 in [0, 1], half 1 in [2, 3]
+    src = l;
+    wave_sort64(key, src);
+    gather(src);
+}
+
 __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ xyz_in, int dim,
-                                                      const int32_t* __restrict__ perm, TileInfo* tiles, int ntiles,
+                                                      int32_t* __restrict__ perm, TileInfo* tiles, int ntiles,
                                                       double* xyz64, float4* rel32, int32_t* inv,
                                                       unsigned* rho_bits) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -193,9 +240,14 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
     const bool v = l < count;
     const int i = start + l;
     double p[3] = {0, 0, 0};
+    int o = 0;
     if (v) {
-        const int o = perm[i];
+        o = perm[i];
         for (int a = 0; a < dim; ++a) p[a] = xyz_in[(int64_t)o * dim + a];
+    }
+    split_order(p, o, dim, v);   // valid rows stay in lanes 0 .. count-1
+    if (v) {
+        perm[i] = o;
         inv[o] = i;
         double4 q;
         q.x = p[0];
@@ -2119,7 +2171,7 @@ hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& 
     return hipGetLastError();
 }
 
-hipError_t launch_build_tiles(const double* xyz_in, int dim, const int32_t* perm, TileInfo* tiles, int ntiles,
+hipError_t launch_build_tiles(const double* xyz_in, int dim, int32_t* perm, TileInfo* tiles, int ntiles,
                               double* xyz64, float4* rel32, int32_t* inv, unsigned* rho_bits, hipStream_t st) {
     const unsigned g = (unsigned)((ntiles + kWavesPerWG - 1) / kWavesPerWG);
     hipLaunchKernelGGL(k_build_tiles, dim3(g), dim3(256), 0, st, xyz_in, dim, perm, tiles, ntiles, xyz64, rel32, inv,
