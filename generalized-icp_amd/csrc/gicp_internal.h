@@ -25,7 +25,14 @@ constexpr int kCorrWaves = GICP_CORR_WAVES;       // waves per k_corr workgroup
 
 constexpr int kListMax = 64;       // candidate target tiles kept per source tile
 constexpr int kPoseRing = 64;      // passes a list stays usable for
-constexpr int kSub = 4;            // 16-row sub-tiles per tile (finer culling of the row scan)
+#ifndef GICP_SUB_TILES
+#define GICP_SUB_TILES 4
+#endif
+// sub-tiles per tile (finer culling of the row scan).  8 (8-row sub-tiles) screens 27-38 % fewer
+// rows on the 1M bench but ran 2 % slower: twice the sub-box tests, and the tile metadata no longer
+// fits k_corr's scalar registers (44 SGPRs spilled)
+constexpr int kSub = GICP_SUB_TILES;
+constexpr int kSubRows = 64 / kSub;    // rows per sub-tile (a multiple of 4: the scan's row group)
 constexpr int kOrderBuckets = 16;  // cost classes of the longest-first workgroup order
 
 struct __attribute__((aligned(16))) TileInfo {
@@ -34,7 +41,7 @@ struct __attribute__((aligned(16))) TileInfo {
     int32_t start;    // first sorted point
     int32_t count;    // 1..64
     float radius;     // max |rel32| norm
-    float sc[3][kSub];  // sub-tile box centres (rows 16g..16g+15) relative to c, fp32, axis-major
+    float sc[3][kSub];  // sub-tile box centres (rows kSubRows g ..) relative to c, fp32, axis-major
     float sh[3][kSub];  // sub-tile box half-extents (cover every rel32 of the sub-tile), axis-major
 };
 

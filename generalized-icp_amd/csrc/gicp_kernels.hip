@@ -182,51 +182,37 @@ __global__ void k_morton(const double* __restrict__ xyz, int64_t n, int dim, Dev
 
 // One wave per tile: gather the tile's points (original order -> sorted), fp64 AABB,
 // centre, fp32 relative coordinates, half-extents and radius.
-// Order of the rows inside a tile: a two-level median split instead of the Morton order the tile
-// was cut from.  Rows 0-31 / 32-63 are the halves along the tile's longest axis, and each half is
-// ordered along its own longest axis, so the four 16-row sub-tiles are compact boxes (a Morton run
-// of 16 can straddle a cell boundary and span the whole tile).  Rows carry no meaning beyond the
+// Order of the rows inside a tile: a recursive median split instead of the Morton order the tile
+// was cut from.  Rows 0-31 / 32-63 are the halves along the tile's longest axis, each half is split
+// along its own longest axis, and so on down to the sub-tile size, so the sub-tiles are compact
+// boxes (a Morton run can straddle a cell boundary and span the whole tile).  Rows carry no meaning beyond the
 // sub-tile boxes (ties are resolved on original indices), so only the culling changes.
 __device__ __forceinline__ void split_order(double (&p)[3], int& o, int dim, bool v) {
     const int l = lane_id();
-    auto longest = [&](const double* mn, const double* mx) {
+    const int cnt = __popcll(__ballot(v));   // valid rows are lanes 0 .. cnt-1, and stay there
+    const bool vv = l < cnt;
+    // each level halves every segment of `seg` rows along that segment's own longest axis
+    for (int seg = kTile; seg > kSubRows; seg >>= 1) {
+        double mn[3], mx[3];
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = vv ? p[a] : 1e300;
+            mx[a] = vv ? p[a] : -1e300;
+            for (int s = 1; s < seg; s <<= 1) {   // xor offsets below seg stay inside the segment
+                mn[a] = fmin(mn[a], __shfl_xor(mn[a], s));
+                mx[a] = fmax(mx[a], __shfl_xor(mx[a], s));
+            }
+        }
         int ax = 0;
         for (int a = 1; a < dim; ++a)
             if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
-        return ax;
-    };
-    auto gather = [&](int src) {
+        const double span = mx[ax] - mn[ax];
+        const float t = span > 0.0 ? (float)((p[ax] - mn[ax]) / span) : 0.f;
+        float key = vv ? (float)(2 * (l / seg)) + t : 3e38f;   // segment s keeps keys in [2s, 2s + 1]
+        int src = l;
+        wave_sort64(key, src);
         for (int a = 0; a < 3; ++a) p[a] = __shfl(p[a], src);
         o = __shfl(o, src);
-    };
-    double mn[3], mx[3];
-    for (int a = 0; a < 3; ++a) {
-        mn[a] = wave_mind(v ? p[a] : 1e300);
-        mx[a] = wave_maxd(v ? p[a] : -1e300);
     }
-    const int ax = longest(mn, mx);
-    float key = v ? (float)(p[ax] - mn[ax]) : 3e38f;   // invalid rows sort last
-    int src = l;
-    wave_sort64(key, src);
-    gather(src);
-    // second level: each 32-row half along its own longest axis (xor offsets < 32 stay in the half)
-    const int cnt = __popcll(__ballot(v));
-    const bool vv = l < cnt;
-    for (int a = 0; a < 3; ++a) {
-        mn[a] = vv ? p[a] : 1e300;
-        mx[a] = vv ? p[a] : -1e300;
-        for (int s = 1; s < 32; s <<= 1) {
-            mn[a] = fmin(mn[a], __shfl_xor(mn[a], s));
-            mx[a] = fmax(mx[a], __shfl_xor(mx[a], s));
-        }
-    }
-    const int ax2 = longest(mn, mx);
-    const double span = mx[ax2] - mn[ax2];
-    const float t = span > 0.0 ? (float)((p[ax2] - mn[ax2]) / span) : 0.f;
-    key = vv ? (float)(2 * (l >> 5)) + t : 3e38f;   // half 0 in [0, 1], half 1 in [2, 3]
-    src = l;
-    wave_sort64(key, src);
-    gather(src);
 }
 
 __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ xyz_in, int dim,
@@ -268,18 +254,18 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
     float h[3];
     for (int a = 0; a < 3; ++a) h[a] = wave_maxf(fabsf(r[a]));
     const float rad = wave_maxf(sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]));
-    // 16-row sub-tile boxes (min/max over each 16-lane row of the wave)
+    // sub-tile boxes (min/max over each kSubRows-lane segment of the wave)
     float smn[3], smx[3];
     for (int a = 0; a < 3; ++a) {
         smn[a] = v ? r[a] : 3e38f;
         smx[a] = v ? r[a] : -3e38f;
-        for (int o = 1; o < 16; o <<= 1) {
+        for (int o = 1; o < kSubRows; o <<= 1) {
             smn[a] = fminf(smn[a], __shfl_xor(smn[a], o));
             smx[a] = fmaxf(smx[a], __shfl_xor(smx[a], o));
         }
     }
-    if ((l & 15) == 0) {
-        const int g = l >> 4;
+    if (l % kSubRows == 0) {
+        const int g = l / kSubRows;
         TileInfo& t = tiles[T];
         for (int a = 0; a < 3; ++a) {
             const bool empty = smn[a] > smx[a];
@@ -573,19 +559,19 @@ __device__ __forceinline__ void scan_group(const WaveLds& L, const float* pr, un
 template <int D, class Row, int... G>
 __device__ __forceinline__ void scan_groups(const WaveLds& L, int n4, unsigned sub, const float* pr, unsigned M,
                                             Row& row, std::integer_sequence<int, G...>) {
-    // short-circuit fold: group G runs only while 4G < n4; skipped when its 16-row sub-tile is not needed
-    (void)((4 * G < n4 ? (((sub >> (G / 4)) & 1u) ? scan_group<4 * G, D>(L, pr, M, row) : void(), true) : false) &&
+    // short-circuit fold: group G runs only while 4G < n4; skipped when its sub-tile is not needed
+    (void)((4 * G < n4 ? (((sub >> (4 * G / kSubRows)) & 1u) ? scan_group<4 * G, D>(L, pr, M, row) : void(), true) : false) &&
            ...);
 }
 
-// Per-lane squared gap to each 16-row sub-box of the staged tile; bit g of the result is set when
+// Per-lane squared gap to each sub-box of the staged tile; bit g of the result is set when
 // some lane within its bound needs sub-tile g.  Same conservative slack as lane_gap2.
 template <int D>
 __device__ __forceinline__ unsigned sub_mask(const TileInfo& ti, const float* pr, bool valid, float bound) {
     unsigned m = 0;
 #pragma unroll
     for (int g = 0; g < kSub; ++g) {
-        if (16 * g >= ti.count) break;
+        if (kSubRows * g >= ti.count) break;
         float g2 = 0.f;
 #pragma unroll
         for (int a = 0; a < D; ++a) {
@@ -621,7 +607,7 @@ __device__ __forceinline__ unsigned sub_mask_ns(const TileInfo& ti, const float*
     unsigned m = 0;
 #pragma unroll
     for (int g = 0; g < kSub; g += 2) {
-        if (16 * g >= ti.count) break;
+        if (kSubRows * g >= ti.count) break;
         f2v g2 = {0.f, 0.f};
 #pragma unroll
         for (int a = 0; a < D; ++a) {
@@ -631,7 +617,7 @@ __device__ __forceinline__ unsigned sub_mask_ns(const TileInfo& ti, const float*
             g2 = __builtin_elementwise_fma(gg, gg, g2);
         }
         if (wave_any(g2.x <= bound)) m |= 1u << g;
-        if (16 * (g + 1) < ti.count && wave_any(g2.y <= bound)) m |= 2u << g;
+        if (kSubRows * (g + 1) < ti.count && wave_any(g2.y <= bound)) m |= 2u << g;
     }
     return m;
 }
@@ -640,14 +626,14 @@ __device__ __forceinline__ int rows_scanned(unsigned sub, int count) {
     int r = 0;
 #pragma unroll
     for (int g = 0; g < kSub; ++g)
-        if ((sub >> g) & 1u) r += min(16, max(0, ((count + 3) & ~3) - 16 * g));
+        if ((sub >> g) & 1u) r += min(kSubRows, max(0, ((count + 3) & ~3) - kSubRows * g));
     return r;
 }
 
 // Scan one staged tile: row(key, j) for every row of the sub-tiles in `sub`; key = (d2 bits & ~63) | row.
 template <int D, class Row>
 __device__ __forceinline__ void scan_tile(const WaveLds& L, int count, const float* pr, Row&& row,
-                                          unsigned sub = 0xFu) {
+                                          unsigned sub = 0xFFFFFFFFu) {
     const unsigned M = key_mask();
     scan_groups<D>(L, (count + 3) & ~3, sub, pr, M, row, std::make_integer_sequence<int, kTile / 4>{});
 }
@@ -1390,9 +1376,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 wave_sync();
                 for (int g = 0; g < kSub; ++g) {
                     if (!((sub >> g) & 1u)) continue;
-                    const int je = min(16 * g + 16, ti.count);
+                    const int je = min(kSubRows * g + kSubRows, ti.count);
 #pragma unroll 4
-                    for (int jj = 16 * g; jj < je; ++jj) {
+                    for (int jj = kSubRows * g; jj < je; ++jj) {
                         const double qq[3] = {L.t.x64[jj], L.t.y64[jj], L.t.z64[jj]};
                         const double d2 = dist2_exact<D>(qq, q.p64);
                         const int og = L.t.perm[jj];
