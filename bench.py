@@ -3,8 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n POINTS] [--dim 3]
 
 A step is one outer GICP iteration (gicp.py:116-167): correspondences + weights +
-statistics on the GPU (k_corr + k_reduce), the RCCL all-reduce of the 74 fp64
-statistics when N > 1, and the host pose solve.  Default workload = BASELINE.json
+statistics on the GPU (k_corr, reduced inside the launch), the RCCL all-reduce of the 77
+fp64 statistics when N > 1, and the pose solve + convergence test on the device (k_solve).
+Default workload = BASELINE.json
 configs[2]: two synthetic 3-D clouds of 1M points, k = 20 covariances, d_c = 0.5 m,
 d_n = 1.0 m; with --gpus N the source is sharded over N ranks (configs[3]).
 Convergence is disabled so every run does exactly K iterations.

@@ -1554,9 +1554,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         d4v acc = {0.0, 0.0, 0.0, 0.0};
         WaveStat& X = s_lds[w].st;
         const int row = l & 15;
+        // points that contribute nothing (rejected, or the tile's padding lanes) have u = v = 0: a group
+        // of 16 or an MFMA's 4 points with none accepted adds exact zeros and is skipped (uniform test)
+        const uint64_t onm = __ballot(on);
         wave_sync();
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
+            if (((onm >> (16 * g)) & 0xFFFFull) == 0) continue;
             if ((l >> 4) == g) {
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
@@ -1568,6 +1572,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             wave_sync();
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
+                if (((onm >> (16 * g + 4 * cc)) & 0xFull) == 0) continue;
                 const int r = 4 * cc + (l >> 4);
                 const int e = l & 15;
                 const int off = r * 16 + 2 * ((e >> 1) ^ (r & 7)) + (e & 1);
