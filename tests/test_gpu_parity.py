@@ -287,13 +287,15 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
     A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
     default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
-    certificates or lists (plain full walks), while the certified passes evaluate far fewer pairs."""
+    certificates or lists (plain full walks), and one with the longest-first workgroup order, while the
+    certified passes evaluate far fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1", "plain"):
-        monkeypatch.setenv("GICP_NO_CERTS", "0" if flag == "0" else "1")
+    for flag in ("0", "1", "plain", "ordered"):
+        monkeypatch.setenv("GICP_NO_CERTS", "1" if flag in ("1", "plain") else "0")
         monkeypatch.setenv("GICP_NO_LISTS", "1" if flag == "plain" else "0")
+        monkeypatch.setenv("GICP_NO_ORDER", "0" if flag == "ordered" else "1")   # longest-first launch order
         e = gicp.Engine(0)
         try:
             e.set_target(tgt, p)
@@ -309,7 +311,7 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    for other in ("1", "plain"):
+    for other in ("1", "plain", "ordered"):
         assert np.array_equal(out["0"][0], out[other][0])
         for a, b in zip(out["0"][1], out[other][1]):
             assert np.array_equal(a, b)
