@@ -134,15 +134,19 @@ def main():
     params.max_iterations = max(1, a.warmup)
     eng.align(None, params)
     params.max_iterations = a.steps
+    # the timed run records no HIP events (an event pair costs queue time); the kernel is timed by
+    # the separate runs below.  GICP_BENCH_EVENTS=1 keeps the every-8th-launch pairs in the timed run.
+    params.timing_stride = 0 if os.environ.get("GICP_BENCH_EVENTS") == "1" else -1
     sync()
     t1 = time.perf_counter()
     T, res = eng.align(None, params)
     sync()
     elapsed = time.perf_counter() - t1
-    # kernel timing runs (not the metric): the timed run samples every 8th k_corr launch with HIP
-    # events (an event pair around every launch adds queue work), and the launch cost falls ~4x as
-    # the pose converges, so one sample set is biased; 8 more identical K-iteration runs with the
-    # sampling offset 0..7 time every launch once, each at the production stride
+    params.timing_stride = 0
+    # kernel timing runs (not the metric): an event pair around every launch adds queue work, so each
+    # run samples every 8th k_corr launch, and the launch cost falls ~4x as the pose converges, so one
+    # sample set is biased; 8 identical K-iteration runs with the sampling offset 0..7 time every
+    # launch once
     corr_ms_total = 0.0
     timed = 0
     for off in range(8):

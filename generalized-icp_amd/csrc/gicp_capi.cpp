@@ -1060,7 +1060,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         hs.converged_at = -1;
         HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
         const int grid = corr_grid(c->src.ntiles, c->shard, c->nshards);
-        const bool timing = res != nullptr;
+        const bool timing = res != nullptr && prm.timing_stride >= 0;   // < 0: no timing events
         const auto t0 = std::chrono::steady_clock::now();
         double corr_ms = 0.0;
         int enq = 0, samples = 0;

@@ -57,7 +57,8 @@ typedef struct gicp_params {
     int32_t fixed_iterations;               /* 1: never stop on tolerance (benchmark mode) */
     int32_t min_neighbors;                  /* 0 -> dim (2-D: > 1 neighbour, gicp.py:27) */
     int32_t timing_stride;                  /* gicp_align times every n-th correspondence launch with HIP
-                                               events (0 -> 8; 1 = every launch, adds queue work) ... */
+                                               events (0 -> 8; 1 = every launch, adds queue work;
+                                               < 0: no events, corr_kernel_ms 0) ... */
     int32_t timing_offset;                  /* ... starting at launch timing_offset (< stride) */
     /* --- additions beyond gicp.py; zero = the reference's behaviour --- */
     int32_t cov_model;                      /* GICP_COV_* : which covariances weight a correspondence
