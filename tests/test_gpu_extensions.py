@@ -189,3 +189,19 @@ def test_gicp_full_output_top5_vs_oracle():
         assert np.all(d < 1e-6)
         np.testing.assert_allclose(np.sort(det[sel]), np.sort(det)[-5:], rtol=1e-9)
         np.testing.assert_allclose(out[5][it], r["q"][sel], atol=1e-9)
+
+
+def test_align_without_timing_events_is_identical(eng, scene3d):
+    """timing_stride < 0 (bench.py's timed run) records no HIP events: the same pose and statistics,
+    no sampled kernel time; the default stride samples every 8th launch."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=12, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    T_ev, r_ev = eng.align(None, p)
+    p.timing_stride = -1
+    T_no, r_no = eng.align(None, p)
+    assert np.array_equal(T_ev, T_no)
+    assert r_no["final_loss"] == r_ev["final_loss"] and r_no["iterations"] == r_ev["iterations"] == 12
+    assert r_no["corr_samples"] == 0 and r_no["corr_kernel_ms"] == 0.0
+    assert r_ev["corr_samples"] == 2 and r_ev["corr_kernel_ms"] > 0.0
