@@ -9,6 +9,13 @@ Default workload = BASELINE.json
 configs[2]: two synthetic 3-D clouds of 1M points, k = 20 covariances, d_c = 0.5 m,
 d_n = 1.0 m; with --gpus N the source is sharded over N ranks (configs[3]).
 Convergence is disabled so every run does exactly K iterations.
+
+The timed registration starts COLD: the engine's pose-dependent caches (candidate lists,
+nearest-neighbour certificates, last matches) are dropped after the warmup (gicp_reset_cache), so
+the K iterations pay the first full walks from the identity exactly as a fresh registration does.
+roofline.achieved follows SURVEY.md §8(d): algorithmic bytes per k_corr launch
+B = 24 (N/G + M) (fp32 xyz + fp32 normal of every source point of the shard and every target
+point, read once) over the HIP-event mean k_corr duration.
 """
 import argparse
 import json
@@ -25,7 +32,8 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md, HBM3E peak
 FP32_PEAK_TFLOPS = 157.3     # MI355X vector FP32 peak
-BYTES_PER_POINT = 80         # fp32 screen (16) + fp64 xyz (32) + covariance (32)
+BYTES_PER_POINT = 24         # SURVEY.md §8(d) contract: fp32 xyz (12) + fp32 unit normal (12), read once
+IMPL_BYTES_PER_POINT = 80    # DESIGN.md §3 layout actually read: fp32 screen (16) + fp64 xyz (32) + covariance (32)
 FLOP_PER_PAIR = 8            # 3 sub + 1 mul + 2 fma (counted as 2) in the fp32 screen
 
 
@@ -37,7 +45,10 @@ def parse():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=16,
+                    help="cKDTree workers of the CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--warm", action="store_true",
+                    help="diagnostic: time the registration warm (caches left by the warmup), not the metric")
     ap.add_argument("--shard-sim", type=int, default=1,
                     help="diagnostic: one process runs only shard 0 of S (no collective) to time a rank of an "
                          "S-GPU job; the line is marked and is not the metric")
@@ -105,7 +116,8 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        local = local % max(1, torch.cuda.device_count())   # rehearsal on fewer GPUs than ranks
+        if local >= torch.cuda.device_count():   # RCCL refuses two ranks on one GPU
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPUs")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import gicp
@@ -137,11 +149,20 @@ def main():
     # the timed run records no HIP events (an event pair costs queue time); the kernel is timed by
     # the separate runs below.  GICP_BENCH_EVENTS=1 keeps the every-8th-launch pairs in the timed run.
     params.timing_stride = 0 if os.environ.get("GICP_BENCH_EVENTS") == "1" else -1
+    if not a.warm:
+        eng.reset_cache()   # cold start: nothing inherited from the warmup
     sync()
     t1 = time.perf_counter()
     T, res = eng.align(None, params)
     sync()
     elapsed = time.perf_counter() - t1
+    warm_elapsed = None
+    if not a.warm:   # diagnostic: the same registration again, continuing from the caches it left
+        sync()
+        t2 = time.perf_counter()
+        eng.align(None, params)
+        sync()
+        warm_elapsed = time.perf_counter() - t2
     params.timing_stride = 0
     # kernel timing runs (not the metric): an event pair around every launch adds queue work, so each
     # run samples every 8th k_corr launch, and the launch cost falls ~4x as the pose converges, so one
@@ -149,18 +170,27 @@ def main():
     # launch once
     corr_ms_total = 0.0
     timed = 0
+    per_iter = np.full(a.steps, np.nan)
     for off in range(8):
         params.timing_offset = off
+        if not a.warm:
+            eng.reset_cache()   # every timing run starts cold, as the timed run did
         _, res_t = eng.align(None, params)
         corr_ms_total += res_t["corr_kernel_ms_sampled"]
         timed += res_t["corr_samples"]
+        t_it = eng.iteration_times()
+        got = ~np.isnan(t_it)
+        per_iter[:len(t_it)][got] = t_it[got]
     params.timing_offset = 0
     assert timed == a.steps, (timed, a.steps)
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, corr_ms_total], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, corr_ms_total, warm_elapsed or 0.0, *per_iter], dtype=torch.float64,
+                         device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, corr_ms_total = float(t[0]), float(t[1])
+        warm_elapsed = float(t[2]) or None
+        per_iter = t[3:].cpu().numpy()
     if dist is not None:   # every rank releases its communicator, then the process group
         eng.close()
         dist.barrier()
@@ -172,7 +202,9 @@ def main():
     n_shard = a.n / max(world, a.shard_sim)
     corr_avg_ms = corr_ms_total / a.steps
     alg_bytes = BYTES_PER_POINT * (n_shard + a.n)
+    impl_bytes = IMPL_BYTES_PER_POINT * (n_shard + a.n)
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
+    n_mov = min(10, a.steps)
     pairs = res["pairs_total"] / a.steps / world   # mean per launch (summed over ranks by the all-reduce)
     traffic, traffic_src = measured_traffic(name) if world == 1 else (None, None)
     line = {
@@ -187,15 +219,28 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32-screen+f64",
-        "data": "synthetic (3-D room scene of SURVEY.md §8(d), area-uniform samples, 5 mm noise)",
+        "data": ("synthetic (3-D room scene of SURVEY.md §8(d), area-uniform samples, 5 mm noise)" if a.dim == 3
+                 else "synthetic (2-D segment scene of BASELINE.md §3, 0.5 px noise)"),
         "config": {"workload": name, "n_source": a.n, "n_target": a.n, "dim": a.dim,
                    "k": 20 if a.dim == 3 else 6, **kw,
                    "parallelism": f"dp{world} (source shards; RCCL all-reduce of 74 fp64 per iteration)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_corr", "kernel_avg_ms": corr_avg_ms, "alg_bytes_per_launch": alg_bytes,
-                     "kernel_timing": "HIP events, every k_corr launch of K timed once (8 identical K-iteration "
-                                      "runs at sampling offsets 0..7, stride 8)"},
+                     "alg_bytes_rule": "SURVEY.md 8(d): 24 B x (N/G + M)",
+                     "impl_bytes_per_launch": impl_bytes,
+                     "impl_frac": impl_bytes / (corr_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_timing": "HIP events, every k_corr launch of K timed once (8 identical cold-start "
+                                      "K-iteration runs at sampling offsets 0..7, stride 8)"},
+        "passes": {"moving_pass_us": float(np.mean(per_iter[:n_mov])) * 1e3,
+                   "converged_pass_us": float(np.mean(per_iter[-n_mov:])) * 1e3,
+                   "first_pass_us": float(per_iter[0]) * 1e3,
+                   "k_corr_us_per_iteration": [round(float(x) * 1e3, 1) for x in per_iter],
+                   "note": "moving = mean k_corr of iterations 1-10 (the pose still moves), converged = last 10"},
+        "warm_start": None if warm_elapsed is None else
+        {"value": a.steps / warm_elapsed, "ms_per_step": warm_elapsed * 1e3 / a.steps,
+         "note": "diagnostic, not the metric: the same K iterations again, continuing from the caches"},
+        "start": "warm (diagnostic)" if a.warm else "cold (caches reset after the warmup)",
         "valu": {"pairs_per_launch": pairs, "tflops": pairs * FLOP_PER_PAIR / (corr_avg_ms * 1e-3) / 1e12,
                  "peak_tflops": FP32_PEAK_TFLOPS,
                  "frac": pairs * FLOP_PER_PAIR / (corr_avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
@@ -213,9 +258,12 @@ def main():
         try:
             its, setup, dt = cpu_baseline(src, tgt, kw, a.cpu_workers)
             line["cpu_baseline"] = {"value": its, "unit": "it/s", "cores": a.cpu_workers, "kind": "port",
-                                    "sample": f"oracle (NumPy/SciPy cKDTree workers={a.cpu_workers}) on the same "
-                                              f"{name} clouds, 1 outer iteration after {setup:.1f} s setup "
-                                              f"(covariances), {dt:.1f} s timed"}
+                                    "host_nproc": os.cpu_count(),
+                                    "sample": f"oracle (NumPy/SciPy cKDTree workers={a.cpu_workers}; host nproc "
+                                              f"{os.cpu_count()}, of which this job's share is {a.cpu_workers}) on "
+                                              f"the same {name} clouds, 1 outer iteration after {setup:.1f} s "
+                                              f"setup (covariances), {dt:.1f} s timed; parity of the 3-D oracle is "
+                                              f"pinned by its 2-D instance (reference fixtures) + ground truth"}
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"value": None, "error": repr(e)}
     else:

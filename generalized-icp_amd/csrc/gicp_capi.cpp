@@ -33,6 +33,7 @@ hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipSt
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t);
+hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, int64_t, int, double*, int32_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
 int corr_grid(int q_tiles, int shard, int nshards);
@@ -209,6 +210,12 @@ struct gicp_ctx {
     double last_rebuilds = 0.0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    gicp_allreduce_fn hook = nullptr;  // host statistics exchange (gicp_set_allreduce)
+    void* hook_user = nullptr;
+    double* h_xchg = nullptr;         // pinned exchange buffer of the hook
+    std::vector<float> iter_ms;       // sampled k_corr time per iteration of the last align (-1: not sampled)
+    double* d_rot = nullptr;          // gicp_rotated_covariances output
+    size_t cap_rot = 0;
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
     // diagnostics of the last pass
@@ -630,8 +637,15 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
 }
 
 void allreduce_stats(gicp_ctx* c) {
-    if (!c->comm) return;
     const int nsx = nstat_ext(c->src.dim);
+    if (c->hook) {   // host exchange: statistics out, the caller's sum over ranks back in
+        HIPCHK(hipMemcpyAsync(c->h_xchg, c->d_state->stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->hook(c->h_xchg, nsx, c->hook_user) != 0) throw Fail{GICP_E_COMM, "host all-reduce hook failed"};
+        HIPCHK(hipMemcpyAsync(c->d_state->stats, c->h_xchg, sizeof(double) * nsx, hipMemcpyHostToDevice, c->stream));
+        return;
+    }
+    if (!c->comm) return;
     ncclResult_t r = ncclAllReduce(c->d_state->stats, c->d_state->stats, nsx, ncclFloat64, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
 }
@@ -874,6 +888,8 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->s_idx);
     dfree(c->s_sort);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_xchg) (void)hipHostFree(c->h_xchg);
+    dfree(c->d_rot);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -898,6 +914,7 @@ int gicp_comm_init(gicp_ctx* c, int nranks, int rank, const char id[GICP_COMM_ID
             ncclCommDestroy(c->comm);
             c->comm = nullptr;
         }
+        c->hook = nullptr;   // one exchange per context
         // a one-rank communicator is created too: the all-reduce then runs (as an identity) on the
         // same stream path as a multi-GPU job, which is how the one-GPU tests exercise it
         ncclUniqueId uid;
@@ -1068,12 +1085,15 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         // every launch inserts a few microseconds of queue work per iteration.
         const int kEvStride = prm.timing_stride > 0 ? std::min(prm.timing_stride, (int)gicp_ctx::kMaxBatch) : 8;
         const int kEvOffset = std::max(0, prm.timing_offset) % kEvStride;
+        c->iter_ms.assign((size_t)std::max(0, prm.max_iterations), -1.f);
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
         // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
         // After convergence the remaining launches of a batch exit at once.
         while (enq < prm.max_iterations) {
+            // a host exchange synchronises every iteration anyway: batches of one, so the loop stops
+            // at the converged iteration without launching more
             const int B = std::min(prm.max_iterations - enq,
-                                   prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 4);
+                                   c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 4);
             for (int b = 0; b < B; ++b) {
                 CorrArgs a = corr_args(c, 0);
                 const bool ev = timing && (enq + b) % kEvStride == kEvOffset;
@@ -1093,12 +1113,14 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
                     if (enq - B + b >= hs.iter) break;   // launched after convergence: exited at once
                     float ms = 0.f;
                     HIPCHK(hipEventElapsedTime(&ms, c->ev[2 * b], c->ev[2 * b + 1]));
+                    c->iter_ms[enq - B + b] = ms;
                     corr_ms += ms;
                     ++samples;
                 }
             if (hs.converged) break;
         }
         const auto t1 = std::chrono::steady_clock::now();
+        c->iter_ms.resize((size_t)std::max(0, std::min(hs.iter, prm.max_iterations)));
         if (hs.solve_fail) throw Fail{GICP_E_INVALID, "pose solve failed (degenerate statistics)"};
         std::memcpy(T_out, hs.T, sizeof(double) * n1 * n1);
         if (res) {
@@ -1127,6 +1149,51 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             r.mse = hs.mse;
             *res = r;
         }
+    });
+}
+
+int gicp_reset_cache(gicp_ctx* c) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_reset_cache", [&] {
+        reset_tile_state(c);
+        HIPCHK(hipStreamSynchronize(c->stream));
+    });
+}
+
+int gicp_iteration_times(gicp_ctx* c, float* out, int n) {
+    if (!c || (!out && n > 0) || n < 0) return GICP_E_INVALID;
+    const int m = std::min(n, (int)c->iter_ms.size());
+    for (int i = 0; i < m; ++i) out[i] = c->iter_ms[i];
+    return m;
+}
+
+int gicp_set_allreduce(gicp_ctx* c, gicp_allreduce_fn fn, void* user) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_set_allreduce", [&] {
+        if (fn && !c->h_xchg) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_xchg), sizeof(double) * 80));
+        if (fn && c->comm) {   // one exchange per context: the hook replaces the communicator
+            HIPCHK(hipStreamSynchronize(c->stream));
+            ncclCommDestroy(c->comm);
+            c->comm = nullptr;
+        }
+        c->hook = fn;
+        c->hook_user = fn ? user : nullptr;
+    });
+}
+
+int gicp_rotated_covariances(gicp_ctx* c, int which, const double* R, double* out) {
+    if (!c || !R || !out || (which != 0 && which != 1)) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_rotated_covariances", [&] {
+        Cloud& cl = which == 0 ? c->tgt : c->src;
+        if (!cl.n || !cl.cov_ready) throw Fail{GICP_E_STATE, "cloud not set"};
+        const int d = cl.dim;
+        for (int k = 0; k < d * d; ++k)
+            if (!std::isfinite(R[k])) throw Fail{GICP_E_INVALID, "R contains non-finite values"};
+        const size_t m = (size_t)cl.n * d * d;
+        dreserve(c->d_rot, c->cap_rot, m);
+        HIPCHK(launch_rotate_cov(cl.cov, cl.perm, cl.n, d, R, c->d_rot, c->stream));
+        HIPCHK(hipMemcpyAsync(out, c->d_rot, sizeof(double) * m, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
     });
 }
 

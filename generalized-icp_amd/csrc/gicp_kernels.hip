@@ -2152,8 +2152,49 @@ hipError_t launch_top_weights(const double* det, const int64_t* tgt_index, int64
 }
 
 // ---------------------------------------------------------------------------
+// rotated covariances (gicp.py:120-121 all_source_cov_matrices): R C Rᵀ = a I − (R m)(R m)ᵀ per
+// point, written in original order.  HBM-bound: 36 B read, D² × 8 B written per point.
+// ---------------------------------------------------------------------------
+struct Rot {
+    double r[9];
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) k_rotate_cov(const double4* __restrict__ cov, const int32_t* __restrict__ perm,
+                                                    int64_t n, Rot R, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double4 c = cov[i];
+    const double m[3] = {c.y, c.z, c.w};
+    double rm[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        double v = 0.0;
+#pragma unroll
+        for (int b = 0; b < D; ++b) v = fma(R.r[a * D + b], m[b], v);
+        rm[a] = v;
+    }
+    double* o = out + (int64_t)perm[i] * D * D;
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+        for (int b = 0; b < D; ++b) o[a * D + b] = (a == b ? c.x : 0.0) - rm[a] * rm[b];
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
+hipError_t launch_rotate_cov(const double4* cov, const int32_t* perm, int64_t n, int dim, const double* R, double* out,
+                             hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    Rot r{};
+    for (int k = 0; k < dim * dim; ++k) r.r[k] = R[k];
+    const unsigned g = (unsigned)((n + 255) / 256);
+    if (dim == 2) hipLaunchKernelGGL(k_rotate_cov<2>, dim3(g), dim3(256), 0, st, cov, perm, n, r, out);
+    else hipLaunchKernelGGL(k_rotate_cov<3>, dim3(g), dim3(256), 0, st, cov, perm, n, r, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& fr, uint32_t* codes, int32_t* idx,
                          hipStream_t st) {
     const int bs = 256;

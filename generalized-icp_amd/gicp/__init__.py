@@ -14,13 +14,15 @@ calls gicp() from a forked worker, robot-visualization.py:199).
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 
 import numpy as np
 
 from . import _lib
 from ._lib import Debug, Params, Result, check, dptr
 
-__all__ = ["gicp", "apply_transformation", "Engine", "expand_stats", "stats_size", "default_params"]
+__all__ = ["gicp", "apply_transformation", "Engine", "RotatedCovariances", "expand_stats", "stats_size",
+           "default_params"]
 
 
 def stats_size(dim):
@@ -108,6 +110,8 @@ class Engine:
         self.device = device
         self.dim = None
         self.n_src = self.n_tgt = 0
+        self.generation = 0        # bumped whenever the source cloud changes (lazy covariance views)
+        self._hook = None          # keeps the ctypes callback of set_allreduce alive
 
     def close(self):
         if self._ctx:
@@ -149,11 +153,13 @@ class Engine:
         check(self._lib.gicp_set_source(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p), shard, nshards),
               self._ctx, "gicp_set_source")
         self.n_src, self.dim = a.shape
+        self.generation += 1
 
     def target_to_source(self, shard=0, nshards=1):
         check(self._lib.gicp_target_to_source(self._ctx, shard, nshards), self._ctx, "gicp_target_to_source")
         self.n_src = self.n_tgt
         self.n_tgt = 0
+        self.generation += 1
 
     def covariances(self, which="target"):
         w = 0 if which == "target" else 1
@@ -161,6 +167,55 @@ class Engine:
         out = np.empty((n, self.dim, self.dim))
         check(self._lib.gicp_get_covariances(self._ctx, w, dptr(out)), self._ctx, "gicp_get_covariances")
         return out
+
+    def rotated_covariances(self, R, which="source"):
+        """R C Rᵀ of every point on the device (gicp_rotated_covariances), original order."""
+        w = 0 if which == "target" else 1
+        n = self.n_tgt if w == 0 else self.n_src
+        R = np.ascontiguousarray(np.asarray(R, dtype=np.float64))
+        if R.shape != (self.dim, self.dim):
+            raise ValueError(f"R must be {self.dim} x {self.dim}")
+        out = np.empty((n, self.dim, self.dim))
+        check(self._lib.gicp_rotated_covariances(self._ctx, w, dptr(R), dptr(out)), self._ctx,
+              "gicp_rotated_covariances")
+        return out
+
+    def reset_cache(self):
+        """Forget the pose-dependent caches (lists, certificates, last matches): the next pass starts cold."""
+        check(self._lib.gicp_reset_cache(self._ctx), self._ctx, "gicp_reset_cache")
+
+    def iteration_times(self):
+        """Sampled k_corr time (ms) per iteration of the last align; NaN where not sampled."""
+        buf = (C.c_float * 4096)()
+        m = self._lib.gicp_iteration_times(self._ctx, buf, 4096)
+        check(min(m, 0), self._ctx, "gicp_iteration_times")
+        t = np.array(buf[:m], dtype=np.float64)
+        t[t < 0] = np.nan
+        return t
+
+    def set_allreduce(self, fn):
+        """Host statistics exchange (gicp_set_allreduce): fn(buf) gets this rank's statistics as a
+        float64 array and must return (or write in place) the sum over ranks.  None removes it."""
+        if fn is None:
+            check(self._lib.gicp_set_allreduce(self._ctx, None, None), self._ctx, "gicp_set_allreduce")
+            self._hook = None
+            return
+
+        def _cb(buf, n, _user):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,))
+                r = fn(a)
+                if r is not None and r is not a:
+                    a[:] = np.asarray(r, dtype=np.float64)
+                return 0
+            except Exception:   # an exception must not cross the C boundary
+                import traceback
+                traceback.print_exc()
+                return -1
+
+        cb = _lib.ALLREDUCE_FN(_cb)
+        check(self._lib.gicp_set_allreduce(self._ctx, C.cast(cb, C.c_void_p), None), self._ctx, "gicp_set_allreduce")
+        self._hook = cb
 
     def neighbor_counts(self, which="target"):
         w = 0 if which == "target" else 1
@@ -288,6 +343,44 @@ def _cg_inner_faithful(src, q, W, offset):
 
 _ENGINES = {}
 
+# 2-D clouds up to this size default to mode='faithful' (scipy fmin_cg on the reference's per-point
+# loss, which copies N x 2 x 2 weights to the host every iteration); larger ones to mode='fast'
+FAITHFUL_MAX_POINTS = 5000
+
+
+class RotatedCovariances(Sequence):
+    """all_source_cov_matrices of the fast path (gicp.py:120-121,174), held lazily: element k is
+    R_k C_s,i R_kᵀ for every source point, R_k the rotation of iteration k.  Only the rotations are
+    stored; an element is computed when read -- on the device (gicp_rotated_covariances) while the
+    engine still holds this source cloud, else from the initial covariances on the host (same
+    formula, R C Rᵀ per point).  Behaves as the reference's list for len / indexing / iteration."""
+
+    def __init__(self, engine, init_cov):
+        self._eng = engine
+        self._gen = engine.generation
+        self._init = init_cov
+        self._R = []
+
+    def append_rotation(self, R):
+        self._R.append(np.array(R, dtype=np.float64))
+
+    def __len__(self):
+        return len(self._R)
+
+    def _one(self, R):
+        e = self._eng
+        if e is not None and e._ctx and e.generation == self._gen:
+            return e.rotated_covariances(R, "source")
+        return np.einsum("ab,nbc,dc->nad", R, self._init, R)
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self._one(R) for R in self._R[k]]
+        return self._one(self._R[k])
+
+    def __repr__(self):
+        return f"RotatedCovariances({len(self)} iterations x {len(self._init)} points)"
+
 
 def _engine(device):
     eng = _ENGINES.get(device)
@@ -330,19 +423,20 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
 
     2-D and 3-D clouds (T is 3x3 or 4x4).
 
-    mode='faithful' (2-D default): every iteration the GPU recomputes the source
-      covariances on the transformed source (gicp.py:120) and produces the
-      correspondences and weights; scipy's fmin_cg then minimises the
-      reference's own per-point loss on them (gicp.py:148-154), so the inexact
-      inner stop follows the reference's trajectory.
-    mode='fast' (3-D default, and any large cloud): source covariances are
+    mode='faithful' (default for 2-D clouds of <= FAITHFUL_MAX_POINTS source points): every
+      iteration the GPU recomputes the source covariances on the transformed source
+      (gicp.py:120) and produces the correspondences and weights; scipy's fmin_cg then
+      minimises the reference's own per-point loss on them (gicp.py:148-154), so the
+      inexact inner stop follows the reference's trajectory.
+    mode='fast' (3-D default, and larger 2-D clouds): source covariances are
       rotated (rigid invariance), the GPU reduces the loss to its sufficient
       statistics in one pass, and the inner problem is solved on the host from
       them -- by fmin_cg on the closed form (inner='cg', 2-D) or exactly by
       Newton on SO(d) (inner='newton').
     full_output=False skips the per-point visualisation extras (the three
     lists come back empty), which is what large clouds want.  In 'fast' mode the
-    top-5 det(W) points are selected on the GPU (no per-point copy).
+    top-5 det(W) points are selected on the GPU (no per-point copy) and
+    all_source_cov_matrices is a RotatedCovariances view (computed when read).
 
     method: 'plane_to_plane' (GICP, the reference), 'point_to_point' (ICP: C_s = 0,
       C_t = I) or 'point_to_plane' (C_s = 0, C_t = P^-1), presentation/main.typ:446-455.
@@ -355,7 +449,8 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     d = src.shape[1]
     if tgt.shape[1] != d:
         raise ValueError("source and target must have the same dimension")
-    mode = ("faithful" if d == 2 else "fast") if mode is None else mode
+    if mode is None:
+        mode = "faithful" if d == 2 and len(src) <= FAITHFUL_MAX_POINTS else "fast"
     if mode not in ("faithful", "fast") or (mode == "faithful" and d != 2):
         raise ValueError("mode must be 'fast', or 'faithful' for 2-D clouds")
     inner = ("cg" if d == 2 else "newton") if inner is None else inner
@@ -381,14 +476,17 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     all_T = [T]
     offset = np.array([T[0, 2], T[1, 2], np.arctan2(T[1, 0], T[0, 0])]) if d == 2 else None
     last = np.inf
-    hw_s, hw_t, all_src_cov = [], [], []
+    hw_s, hw_t = [], []
+    all_src_cov = [] if (mode == "faithful" or not full_output) else RotatedCovariances(eng, init_src_cov)
     eye = np.eye(d + 1)
+    moved_source = False   # faithful mode: the engine holds a transformed copy of the source
     for it in range(int(max_iterations)):
         moved = apply_transformation(src, T)                       # gicp.py:119
         if mode == "faithful":
-            if it > 0:
+            if it > 0 or T0 is not None:
                 eng.set_source(moved, p)                           # gicp.py:120, on the GPU
-            cs = eng.covariances("source") if it > 0 else init_src_cov
+                moved_source = True
+            cs = eng.covariances("source") if moved_source else init_src_cov
             if full_output:
                 all_src_cov.append(cs)
             _, dbg = eng.iterate(eye, debug=True)                  # gicp.py:124-145 on the moved cloud
@@ -404,8 +502,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
         else:
             if full_output:
                 st, top_s, top_t, _ = eng.iterate_top(T, 5)     # gicp.py:170 on the device
-                R = T[:d, :d]
-                all_src_cov.append(np.einsum("ab,nbc,dc->nad", R, init_src_cov, R))
+                all_src_cov.append_rotation(T[:d, :d])            # gicp.py:120-121, read lazily
             else:
                 st = eng.iterate(T)
             if inner == "cg":
@@ -448,7 +545,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
             if verbose:
                 print("Converged at iteration", it, f"({stop})")
             break
-    if mode == "faithful":
+    if moved_source:
         eng.set_source(src, p)   # leave the engine holding the untransformed source
     return T, all_T, init_src_cov, target_cov, hw_s, hw_t, all_src_cov
 

@@ -108,7 +108,14 @@ SIGNATURES = {
     "gicp_pass_info": (C.c_int, [_VP, _DP]),
     "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
+    "gicp_reset_cache": (C.c_int, [_VP]),
+    "gicp_iteration_times": (C.c_int, [_VP, C.POINTER(C.c_float), C.c_int]),
+    "gicp_set_allreduce": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),
+    "gicp_rotated_covariances": (C.c_int, [_VP, C.c_int, _DP, _DP]),
 }
+
+# gicp_allreduce_fn: int (*)(double* buf, int n, void* user)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _DP, C.c_int, C.c_void_p)
 
 _lib = None
 

@@ -21,7 +21,10 @@
  *     runs gicp() in a forked worker).
  *   - One context = one GPU = one host thread; one process per GPU.  Ranks
  *     of a multi-GPU job share the per-iteration statistics through an RCCL
- *     all-reduce (gicp_comm_init); every rank then runs the same host solve.
+ *     all-reduce (gicp_comm_init) -- or a host reducer (gicp_set_allreduce) --
+ *     between the correspondence pass and the pose solve; every rank then runs
+ *     the same device solve (k_solve) on bit-identical sums, so no pose
+ *     broadcast is needed.
  */
 #ifndef GICP_HIP_H
 #define GICP_HIP_H
@@ -136,7 +139,9 @@ int gicp_comm_init(gicp_ctx* ctx, int nranks, int rank, const char id[GICP_COMM_
 int gicp_set_target(gicp_ctx* ctx, const double* xyz, int64_t M, int dim, const gicp_params* p);
 /* Source cloud (gicp.py:100,111): the whole cloud is uploaded (its
  * covariance neighbourhoods need every point); this rank reduces only the
- * points of shard `rank` of `nshards` (Morton-contiguous tiles). */
+ * source tiles of shard `shard` of `nshards`: the cloud's Morton-ordered
+ * tiles in chunks of 64, dealt round-robin (chunks shard, shard + nshards, ...;
+ * gicp/distributed.py shard_tiles states the same split). */
 int gicp_set_source(gicp_ctx* ctx, const double* xyz, int64_t N, int dim, const gicp_params* p,
                     int shard, int nshards);
 /* Promote the current target (index + covariances) to be the next source,
@@ -178,8 +183,34 @@ int gicp_top_weights(gicp_ctx* ctx, int k, int64_t* src_out, int64_t* tgt_out, d
  * Pure host code, no GPU needed.  Writes T_out and the minimum. */
 int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_out, double* loss_out);
 
-/* The whole outer loop (gicp.py:116-167) on the GPU + host solver. */
+/* The whole outer loop (gicp.py:116-167) on the GPU: per iteration the correspondence pass
+ * (k_corr), the statistics exchange when sharded, the pose solve + convergence test (k_solve). */
 int gicp_align(gicp_ctx* ctx, const double* T0, const gicp_params* p, double* T_out, gicp_result* res);
+
+/* Drop every pose-dependent cache of the current clouds (candidate lists, nearest-neighbour
+ * certificates, last matches, seed tiles): the next pass starts cold, as after a fresh
+ * gicp_set_source.  Results never depend on the caches (they are exact); only the time does. */
+int gicp_reset_cache(gicp_ctx* ctx);
+
+/* Per-iteration correspondence-kernel time (ms, HIP events) of the last gicp_align: out[i] for
+ * iteration i, -1 where that launch was not sampled (gicp_params.timing_stride / timing_offset).
+ * Returns the number of iterations written (<= n), or a negative GICP_E_*. */
+int gicp_iteration_times(gicp_ctx* ctx, float* out, int n);
+
+/* Host statistics exchange, for a job whose ranks talk over something other than RCCL (e.g. a
+ * gloo process group, or ranks sharing one GPU, which RCCL refuses).  When set, every pass
+ * copies its statistics (n = gicp_stats_size(dim) + GICP_PASS_INFO doubles) to a host buffer,
+ * calls fn(buf, n, user), which must replace buf by the sum over ranks and return 0, and copies
+ * the sum back before the pose solve -- in gicp_iterate and inside gicp_align's loop (which then
+ * synchronises once per iteration).  Replaces an RCCL communicator on the same context.
+ * fn = NULL removes the hook. */
+typedef int (*gicp_allreduce_fn)(double* buf, int n, void* user);
+int gicp_set_allreduce(gicp_ctx* ctx, gicp_allreduce_fn fn, void* user);
+
+/* The source covariances rotated by R (dim x dim, row-major): R C_s R^T = a I - (R m)(R m)^T per
+ * point, computed on the device (gicp.py:120-121 all_source_cov_matrices, rotated instead of
+ * recomputed), ORIGINAL order, [n, dim, dim].  which: 0 = target, 1 = source. */
+int gicp_rotated_covariances(gicp_ctx* ctx, int which, const double* R, double* out);
 
 #ifdef __cplusplus
 }

@@ -205,3 +205,108 @@ def test_align_without_timing_events_is_identical(eng, scene3d):
     assert r_no["final_loss"] == r_ev["final_loss"] and r_no["iterations"] == r_ev["iterations"] == 12
     assert r_no["corr_samples"] == 0 and r_no["corr_kernel_ms"] == 0.0
     assert r_ev["corr_samples"] == 2 and r_ev["corr_kernel_ms"] > 0.0
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_rotated_covariances_vs_host_einsum(eng, scene3d, dim):
+    """gicp_rotated_covariances (device, a I - (R m)(R m)^T) == R C R^T of the copied covariances
+    (the host einsum gicp.py:120-121 is restated by), original order, to 1e-12 of the entries."""
+    if dim == 3:
+        src, tgt, _ = scene3d
+        p = gicp.default_params(3, **P3)
+        R = _pose()[:3, :3]
+    else:
+        src, tgt, _ = S.segment_scene_2d(5000)
+        p = gicp.default_params(2, max_distance_correspondence=20.0, max_distance_nearest_neighbors=25.0)
+        R = O.rot2(0.3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    for which in ("source", "target"):
+        C0 = eng.covariances(which)
+        ref = np.einsum("ab,nbc,dc->nad", R, C0, R)
+        got = eng.rotated_covariances(R, which)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * np.abs(ref).max())
+
+
+def test_gicp_full_output_rotated_covariances_lazy(scene3d):
+    """all_source_cov_matrices of the fast path (gicp.py:121) is a lazy view: one element per executed
+    iteration, each == R_k C_s R_k^T of that iteration's pose (host einsum, 1e-12), on the device while
+    the engine holds the source and from the initial covariances after it changed."""
+    src, tgt, _ = scene3d
+    kw = dict(max_iterations=4, tolerance=0.0, **P3)
+    T, all_T, init_cov, _, _, _, all_cov = gicp.gicp(src, tgt, verbose=False, **kw)
+    assert isinstance(all_cov, gicp.RotatedCovariances) and len(all_cov) == 4
+    refs = [np.einsum("ab,nbc,dc->nad", Tk[:3, :3], init_cov, Tk[:3, :3]) for Tk in all_T[:4]]
+    for k in range(4):
+        np.testing.assert_allclose(all_cov[k], refs[k], rtol=0, atol=1e-12 * np.abs(refs[k]).max())
+    gicp.gicp(src[:5000], tgt[:5000], verbose=False, full_output=False, **kw)   # the engine's source changes
+    np.testing.assert_allclose(all_cov[-1], refs[-1], rtol=0, atol=1e-12 * np.abs(refs[-1]).max())
+    assert len(list(all_cov)) == 4 and len(all_cov[1:3]) == 2
+
+
+def test_gicp_2d_large_cloud_defaults_to_fast_mode(monkeypatch):
+    """A 2-D 100k call takes mode='fast' (no per-point W / index copied back: every pass is a
+    statistics-only gicp_iterate or the device top-k), and agrees with an explicit mode='fast' call."""
+    src, tgt, _ = S.segment_scene_2d(100_000)
+    kw = dict(max_iterations=6, tolerance=0.0, max_distance_correspondence=20.0, max_distance_nearest_neighbors=25.0)
+    seen = []
+    orig = gicp.Engine.iterate
+
+    def spy(self, T, debug=False):
+        seen.append(debug)
+        return orig(self, T, debug=debug)
+
+    monkeypatch.setattr(gicp.Engine, "iterate", spy)
+    T, all_T, *_ = gicp.gicp(src, tgt, verbose=False, full_output=False, **kw)
+    assert seen and not any(seen), "a large 2-D call copied per-point weights to the host"
+    n_full = len(seen)
+    seen.clear()
+    out = gicp.gicp(src, tgt, verbose=False, **kw)   # full_output: top-5 on the device, lazy covariances
+    assert not any(seen) and isinstance(out[6], gicp.RotatedCovariances)
+    monkeypatch.undo()
+    T2, *_ = gicp.gicp(src, tgt, verbose=False, full_output=False, mode="fast", **kw)
+    np.testing.assert_array_equal(T, T2)
+    assert n_full == len(all_T) - 1
+
+
+@pytest.mark.parametrize("name", ["vis_s3", "robot_p0_r360"])
+def test_gicp_2d_faithful_with_initial_pose_vs_oracle(name):
+    """mode='faithful' with a non-identity T0: the first pass runs on the source moved by T0
+    (gicp.py:119-120), as the oracle does; same endpoint as the oracle's loop, and all_src_cov[0] is
+    the covariance set of the moved cloud."""
+    from golden_util import kwargs, load
+    fx = load(name)
+    T0 = O.offset_to_T(np.array([1.5, -0.8, 0.01]))
+    kw = kwargs(fx)
+    out = gicp.gicp(fx["source"], fx["target"], T0=T0, verbose=False, **kw)
+    ref = O.gicp(fx["source"], fx["target"], T0=T0, **kw)
+    moved0 = O.apply_transformation(fx["source"], T0)
+    cov0, _ = O.covariances(moved0, kw["max_distance_nearest_neighbors"])
+    np.testing.assert_allclose(out[6][0], cov0, atol=1e-10)
+    assert np.allclose(out[1][0], T0)
+    th = lambda T: np.arctan2(T[1, 0], T[0, 0])  # noqa: E731
+    assert abs(th(out[0]) - th(ref[0])) < 1e-4 and np.max(np.abs(out[0][:2, 2] - ref[0][:2, 2])) < 1e-3
+
+
+def test_reset_cache_changes_no_result(eng, scene3d):
+    """gicp_reset_cache drops lists / certificates / last matches: a cold align gives the bit-identical
+    pose and loss of a warm one, and per-iteration kernel times cover every launch over 8 offsets."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=16, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    T_a, r_a = eng.align(None, p)
+    T_w, r_w = eng.align(None, p)        # warm: caches from the first call
+    eng.reset_cache()
+    T_c, r_c = eng.align(None, p)        # cold again
+    assert np.array_equal(T_a, T_w) and np.array_equal(T_a, T_c)
+    assert r_a["final_loss"] == r_w["final_loss"] == r_c["final_loss"]
+    times = np.full(16, np.nan)
+    for off in range(8):
+        p.timing_offset = off
+        eng.reset_cache()
+        eng.align(None, p)
+        t = eng.iteration_times()
+        assert len(t) == 16 and np.sum(~np.isnan(t)) == 2
+        times[~np.isnan(t)] = t[~np.isnan(t)]
+    assert np.all(times > 0)
