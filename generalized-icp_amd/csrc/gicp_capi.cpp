@@ -33,6 +33,7 @@ hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipSt
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t);
+hipError_t launch_graph(const GraphArgs&, int, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, int64_t, int, double*, int32_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
@@ -96,11 +97,14 @@ struct Cloud {
     TileInfo* tiles = nullptr;
     BlockInfo* blocks = nullptr;
     uint32_t* tile_code = nullptr;
+    uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows
+    int32_t* nbi = nullptr;           // ... and their sorted indices
+    bool graph_ready = false;
     bool cov_ready = false;
     int cov_q_begin = 0, cov_q_end = 0;  // tiles whose covariances were computed
 
     size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
-    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0;
+    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0;
     void reserve_points(int64_t np) {
         dreserve(xyz64, cap_xyz, (size_t)np * 4);
         dreserve(rel32, cap_rel, (size_t)np);
@@ -124,9 +128,13 @@ struct Cloud {
         dfree(tiles);
         dfree(blocks);
         dfree(tile_code);
+        dfree(nbq);
+        dfree(nbi);
         cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
+        cap_nbq = cap_nbi = 0;
         n = 0;
         cov_ready = false;
+        graph_ready = false;
     }
     DevCloud view() const {
         DevCloud v{};
@@ -137,6 +145,8 @@ struct Cloud {
         v.tiles = tiles;
         v.blocks = blocks;
         v.tile_code = tile_code;
+        v.nbq = graph_ready ? nbq : nullptr;
+        v.nbi = graph_ready ? nbi : nullptr;
         v.n = n;
         v.ntiles = ntiles;
         v.nblocks = nblocks;
@@ -187,6 +197,7 @@ struct gicp_ctx {
     int32_t* d_cert_pass = nullptr;
     size_t cap_cj = 0, cap_cg = 0, cap_cp = 0;
     bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
+    bool use_graph = true;            // GICP_NO_GRAPH=1: no target neighbour graph, no graph descent
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     // cloud-build scratch and per-source-tile arrays, grow-only (a frame stream allocates once)
     double* s_in = nullptr;
@@ -194,17 +205,13 @@ struct gicp_ctx {
     int32_t* s_idx = nullptr;
     unsigned char* s_sort = nullptr;
     size_t cap_in = 0, cap_codes = 0, cap_codes2 = 0, cap_idx = 0, cap_sort = 0;
-    size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0, cap_order = 0;
+    size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0;
     int cap_k_hint[4] = {0, 0, 0, 0};  // last tile extent-cap step per dimension (tiling warm start)
-    int32_t* d_order = nullptr;       // longest-first unit order (CorrArgs::order)
-    int32_t* d_order_cnt = nullptr;
+    float4* g_nb = nullptr;           // graph build scratch
+    float2* g_nbh = nullptr;
+    size_t cap_gnb = 0, cap_gnbh = 0;
     int pass = 0;
     bool use_lists = true;
-    // longest-first workgroup order within each XCD's unit range from the previous pass's cost
-    // classes: off by default since the search cap / adaptive skin / median-split rows evened out the
-    // waves (identity order measured +1.3 % at 30 iterations, +2.2 % at 200, +2.4 % on one 8-GPU shard);
-    // GICP_NO_ORDER=0 turns it on
-    bool use_order = false;
     double skin_frac = 0.2;           // candidate-list skin as a fraction of d_c (GICP_SKIN)
     double skin_gain = 1.0;           // adaptive skin: multiple of the tile's last displacement (GICP_SKIN_GAIN)
     double last_rebuilds = 0.0;
@@ -219,7 +226,7 @@ struct gicp_ctx {
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
     // diagnostics of the last pass
-    double last_amb = 0.0, last_pairs = 0.0, last_sq = 0.0;
+    double last_amb = 0.0, last_pairs = 0.0, last_sq = 0.0, last_gproved = 0.0, last_walked = 0.0;
     float last_corr_ms = 0.f, last_reduce_ms = 0.f;
     bool timing = false;
 };
@@ -401,7 +408,8 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
 
 // Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
 // is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
-void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p) {
+void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p,
+                 bool graph = false) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -418,6 +426,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     };
     cl.n = 0;   // buffers are kept (grow-only) and reused
     cl.cov_ready = false;
+    cl.graph_ready = false;
     cl.dim = dim;
     cl.bits = dim == 3 ? 10 : 16;
     // one fused, branch-free pass: bounds and the finiteness test (v - v is NaN for NaN and +-inf)
@@ -526,6 +535,24 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         cl.cov_q_begin = qb;
         cl.cov_q_end = qe;
         tick("covariances");
+        if (graph) {   // target neighbour graph for k_corr's graph descent
+            dreserve(cl.nbq, cl.cap_nbq, (size_t)n * 8);
+            dreserve(cl.nbi, cl.cap_nbi, (size_t)n * kGraphK);
+            dreserve(c->g_nb, c->cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
+            dreserve(c->g_nbh, c->cap_gnbh, (size_t)n);
+            GraphArgs ga{};
+            ga.cl = cl.view();
+            ga.mg = ca.mg;
+            ga.search2 = ca.search2;
+            ga.nb = c->g_nb;
+            ga.nbh = c->g_nbh;
+            ga.nbq = cl.nbq;
+            ga.nbi = cl.nbi;
+            HIPCHK(launch_graph(ga, dim, st));
+            HIPCHK(hipStreamSynchronize(st));
+            cl.graph_ready = true;
+            tick("graph");
+        }
         if (verbose)
             std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f | ms:%s\n",
                          (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho, tlog.c_str());
@@ -540,7 +567,6 @@ void reset_tile_state(gicp_ctx* c) {
     HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * nt, c->stream));
     HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
     HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_order_cnt, 0, sizeof(int32_t) * 2 * 8 * kOrderBuckets, c->stream));
     if (c->d_cert_pass) HIPCHK(hipMemsetAsync(c->d_cert_pass, 0xFF, sizeof(int32_t) * nt, c->stream));
     // last matches (k_corr's per-lane search cap): none yet
     if (c->d_cert_j) HIPCHK(hipMemsetAsync(c->d_cert_j, 0xFF, sizeof(int32_t) * std::max<int64_t>(1, c->src.n), c->stream));
@@ -563,9 +589,6 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     dreserve(c->d_cert_j, c->cap_cj, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_gap, c->cap_cg, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_pass, c->cap_cp, nt);
-    const int q8 = std::max(1, corr_grid(c->src.ntiles, c->shard, c->nshards) / 8);
-    dreserve(c->d_order, c->cap_order, (size_t)2 * 8 * kOrderBuckets * q8);
-    if (!c->d_order_cnt) dalloc(c->d_order_cnt, 2 * 8 * kOrderBuckets);
     reset_tile_state(c);
 }
 
@@ -616,8 +639,6 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
         a.cert_pass = c->d_cert_pass;
     }
     a.hint = c->d_hint;
-    a.order = c->use_order ? c->d_order : nullptr;
-    a.order_cnt = c->d_order_cnt;
     a.partials = c->d_partials;
     a.count_pairs = 1;
     a.list = c->d_list;
@@ -771,6 +792,8 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     c->last_pairs = c->h_stats[ns + 1];
     c->last_rebuilds = c->h_stats[ns + 2];
     c->last_sq = c->h_stats[ns + 3];
+    c->last_gproved = c->h_stats[ns + 4];
+    c->last_walked = c->h_stats[ns + 5];
     c->top_ready = a.dbg_det != nullptr;
 }
 
@@ -824,10 +847,10 @@ int gicp_create(gicp_ctx** out, int device) {
     if (!c) return GICP_E_NOMEM;
     c->device = device;
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
-    if (const char* e = std::getenv("GICP_NO_ORDER")) c->use_order = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_NO_GRAPH")) c->use_graph = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -880,13 +903,13 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_list_pass);
     dfree(c->d_list_rcert);
     dfree(c->d_poses);
-    dfree(c->d_order);
-    dfree(c->d_order_cnt);
     dfree(c->s_in);
     dfree(c->s_codes);
     dfree(c->s_codes2);
     dfree(c->s_idx);
     dfree(c->s_sort);
+    dfree(c->g_nb);
+    dfree(c->g_nbh);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_xchg) (void)hipHostFree(c->h_xchg);
     dfree(c->d_rot);
@@ -931,7 +954,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt);
+        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs);
         if (c->src.n) reset_tile_state(c);
     });
 }
@@ -983,6 +1006,35 @@ int gicp_get_covariances(gicp_ctx* c, int which, double* out) {
     });
 }
 
+int gicp_get_graph(gicp_ctx* c, int64_t* index, double* radius) {
+    if (!c) return GICP_E_INVALID;
+    static_assert(GICP_GRAPH_K == kGraphK, "graph width");
+    return guard_impl(c, "gicp_get_graph", [&] {
+        Cloud& cl = c->tgt;
+        if (!cl.n || !cl.graph_ready) throw Fail{GICP_E_STATE, "no target graph (set_target first; GICP_NO_GRAPH unset)"};
+        const int64_t n = cl.n;
+        std::vector<uint4> nbq((size_t)n * 8);
+        std::vector<int32_t> nbi((size_t)n * kGraphK), perm(n);
+        HIPCHK(hipMemcpyAsync(nbq.data(), cl.nbq, sizeof(uint4) * n * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(nbi.data(), cl.nbi, sizeof(int32_t) * n * kGraphK, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(perm.data(), cl.perm, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t o = perm[i];
+            if (radius) {
+                float r;
+                std::memcpy(&r, &nbq[(size_t)i * 8].x, sizeof(float));
+                radius[o] = r;
+            }
+            if (index)
+                for (int k = 0; k < kGraphK; ++k) {
+                    const int t = nbi[(size_t)i * kGraphK + k];
+                    index[o * kGraphK + k] = t >= 0 ? (int64_t)perm[t] : -1;
+                }
+        }
+    });
+}
+
 int gicp_get_neighbor_counts(gicp_ctx* c, int which, int32_t* out) {
     if (!c || !out || (which != 0 && which != 1)) return GICP_E_INVALID;
     return guard_impl(c, "gicp_get_neighbor_counts", [&] {
@@ -1010,6 +1062,8 @@ int gicp_pass_info(gicp_ctx* c, double out[GICP_PASS_INFO]) {
     out[1] = c->last_pairs;
     out[2] = c->last_rebuilds;
     out[3] = c->last_sq;
+    out[4] = c->last_gproved;
+    out[5] = c->last_walked;
     return GICP_OK;
 }
 
@@ -1138,6 +1192,8 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             c->last_pairs = hs.stats_solved[ns + 1];
             c->last_rebuilds = hs.stats_solved[ns + 2];
             c->last_sq = hs.stats_solved[ns + 3];
+            c->last_gproved = hs.stats_solved[ns + 4];
+            c->last_walked = hs.stats_solved[ns + 5];
             r.wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
             // kernel time of the iterations actually executed (after convergence launches exit at once)
             r.corr_kernel_ms = samples ? corr_ms / samples * hs.iter : 0.0;

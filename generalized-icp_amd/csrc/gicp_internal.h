@@ -33,7 +33,12 @@ constexpr int kPoseRing = 64;      // passes a list stays usable for
 // fits k_corr's scalar registers (44 SGPRs spilled)
 constexpr int kSub = GICP_SUB_TILES;
 constexpr int kSubRows = 64 / kSub;    // rows per sub-tile (a multiple of 4: the scan's row group)
-constexpr int kOrderBuckets = 16;  // cost classes of the longest-first workgroup order
+// target neighbour graph: each target point's kGraphK nearest other target points
+constexpr int kGraphK = 20;
+constexpr int kGraphHops = 4;      // descent steps a k_corr lane may take before it walks
+// error bound of the descent's fp32 distances, per metre of the coordinates involved (2^-19: the
+// relative-to-node arithmetic errs by a few 2^-24 per operation)
+constexpr float kGraphErr = 1.9073486328125e-06f;
 
 struct __attribute__((aligned(16))) TileInfo {
     double c[3];      // fp64 centre (midpoint of the fp64 AABB)
@@ -62,6 +67,12 @@ struct DevCloud {
     const TileInfo* tiles;    // [ntiles]
     const BlockInfo* blocks;  // [nblocks] blocks of 64 tiles, then [ceil(nblocks / 64)] super-blocks of 64 blocks
     const uint32_t* tile_code;// [ntiles] Morton code of each tile's first point
+    // neighbour graph (target only; null when not built), DESIGN.md §3c.  Row i is one 128-B line:
+    // dword 0 r(i) (fp32: every target t != i with |x_t - x_i| < r is in the row), dword 1 the scale s,
+    // then kGraphK entries of 3 int16 (x_t - x_i) / s, rounded to nearest (|error| <= s / 2 per
+    // axis); an unused entry has x = -32768.  nbi[i][k] = sorted index of entry k (-1 unused).
+    const uint4* nbq;         // [n][8]
+    const int32_t* nbi;       // [n][kGraphK]
     int64_t n;
     int32_t ntiles;
     int32_t nblocks;
@@ -75,6 +86,17 @@ struct DevCloud {
 struct Margin {
     float a, b, c;
 };
+
+struct GraphArgs {
+    DevCloud cl;
+    float search2;            // fp32 screen bound (d_n^2 + margins): the graph's neighbourhood cap
+    Margin mg;
+    float4* nb;               // [n][kGraphK] scratch: x_t - x_i fp32, t as the w bits
+    float2* nbh;              // [n] scratch: (r, count)
+    uint4* nbq;               // [n][8] out (packed rows)
+    int32_t* nbi;             // [n][kGraphK] out
+};
+static_assert(8 + 6 * kGraphK <= 128, "a graph row is one 128-B line");
 
 struct CovArgs {
     DevCloud cl;
@@ -168,20 +190,14 @@ struct CorrArgs {
     float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
     float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected
     unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
-    // longest-first order: a UNIT is the kCorrWaves consecutive source tiles one
-    // workgroup handles; its partial row and reduction group follow the unit, so the statistics do
-    // not depend on the order.  Units 0 .. 8 q8 - 1 (q8 = units / 8) form 8 contiguous ranges, one
-    // per XCD; within a range the units run in decreasing cost class of the previous pass.
-    // order_cnt[parity][xcd][class], order[parity][xcd][class][q8]; parity = pass & 1 is read,
-    // the other parity is appended to at each workgroup's end (and zeroed after the next pass).
-    int32_t* order;           // null: identity order
-    int32_t* order_cnt;
 };
 
 constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;
 }
 // partials carry extra diagnostics: ambiguous count, pairs evaluated, list rebuilds, sum |r|^2
-constexpr int nstat_ext(int D) { return nstat(D) + 4; }
+// ... and lanes proved by the graph descent, waves that walked (GICP_PASS_INFO)
+constexpr int nstat_ext(int D) { return nstat(D) + 6; }
+static_assert(nstat_ext(3) <= 80, "IterState::stats holds the extended statistics");
 
 }  // namespace gicp

@@ -346,6 +346,27 @@ __device__ __forceinline__ float gap2_box(const Query<D>& q, const double* c, co
     return g2;
 }
 
+// The query box of the lanes where `on` holds (the wave's lanes still searching): their fp32 offsets
+// pw lie within ow' +- ew' (conservative: the centre is rounded, the half-extent padded).  A list
+// walk or fallback tests candidate tiles against it instead of the whole source tile's box, so a
+// wave with a few searching lanes visits only the tiles near them (the list, built for the whole
+// box, covers any subset of its lanes).  Values are shifted by 2 ew (>= |pw|) to use the
+// non-negative wave max; lanes with on = false pass the negative marker.
+template <int D>
+__device__ __forceinline__ Query<D> active_box(const Query<D>& q, bool on) {
+    Query<D> qa = q;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const float B = 2.f * q.ew[a] + 1e-30f;
+        const float hi = wave_maxf(on ? q.pw[a] + B : -1.f) - B;
+        const float lo = B - wave_maxf(on ? B - q.pw[a] : -1.f);
+        const float mid = 0.5f * (lo + hi);
+        qa.ow[a] = q.ow[a] + (double)mid;
+        qa.ew[a] = 0.5f * (hi - lo) + 4.8e-7f * (fabsf(lo) + fabsf(hi) + B) + 1e-30f;
+    }
+    return qa;
+}
+
 // Two-level culled walk over the database tiles.  `visit(T)` returns true when it
 // processed the tile (the wave's bound then shrinks); `wave_bound()` is the max over
 // lanes of the squared search radius still needed.
@@ -913,6 +934,145 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// target neighbour graph: for every target point i its kGraphK nearest other
+// target points (relative positions + sorted indices) and a radius r(i) such that EVERY target
+// t != i with true |x_t - x_i| < r(i) is in the row.  Built once per target cloud; k_corr's graph
+// descent proves nearest neighbours with it.  Only conservativeness of r matters (no tie rules):
+//   phase 1 keeps the K1 = kGraphK + 2 smallest screened keys (self included);
+//   phase 2 emits the rows keyed <= tau = the (kGraphK + 1)-th key, self excluded;
+//   a row not emitted has a screened key > tau, so its true d2 >= key_d2(lk[K1 - 1]) - margin when
+//   that key is above tau (else key_d2(tau) - margin); a lane that found fewer keys than K1 within
+//   the screen radius has every target within it: r2 = search2 - margin.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(256) k_graph(GraphArgs A) {
+    constexpr int KG = kGraphK, K1 = KG + 2;
+    __shared__ WaveLds s_lds[kWavesPerWG];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int T = blockIdx.x * kWavesPerWG + w;
+    if (T >= A.cl.ntiles) return;
+    WaveLds& L = s_lds[w];
+    const DevCloud& cl = A.cl;
+    const TileInfo qt = tile_meta(cl, T);
+    Query<D> q;
+    q.valid = l < qt.count;
+    const int i = qt.start + min(l, qt.count - 1);
+    const float4 rel = cl.rel32[i];
+    const double4 p4 = reinterpret_cast<const double4*>(cl.xyz64)[i];
+    const float relv[3] = {rel.x, rel.y, rel.z};
+    const double p4v[3] = {p4.x, p4.y, p4.z};
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        q.ow[a] = qt.c[a];
+        q.ew[a] = qt.h[a];
+        q.pw[a] = relv[a];
+        q.p64[a] = p4v[a];
+    }
+    const unsigned init = __float_as_uint(A.search2) | 63u;
+    unsigned lk[K1];
+#pragma unroll
+    for (int m = 0; m < K1; ++m) lk[m] = init;
+    auto lane_bound = [&]() -> float { return q.valid ? key_d2(lk[K1 - 1]) : -1.f; };
+    auto visit1 = [&](int Tt) -> bool {
+        const TileInfo ti = tile_meta(cl, Tt);
+        float pr[D];
+        const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
+        if (!__any(need)) return false;
+        stage_f32(cl, ti, L);
+        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
+            if (__any(key < lk[K1 - 1])) {
+#pragma unroll
+                for (int m = K1 - 1; m > 0; --m) lk[m] = umed3(lk[m - 1], lk[m], key);
+                lk[0] = min(lk[0], key);
+            }
+        });
+        wave_sync();
+        return true;
+    };
+    traverse<D>(cl, q, T, visit1, [&]() { return wave_maxf(lane_bound()); });
+
+    const unsigned tau = lk[KG];
+    float r2;
+    if (lk[K1 - 1] >= init) {   // fewer than K1 targets inside the screen radius: all of them are rows
+        r2 = A.search2 - marg(A.mg, A.search2);
+    } else {
+        const float kd = key_d2(lk[K1 - 1] > tau ? lk[K1 - 1] : tau);
+        r2 = kd - marg(A.mg, kd);
+    }
+    const float tau_hi = tau >= init ? A.search2 : __uint_as_float((tau | 63u) + 1u);
+    int cnt = 0;
+    bool over = false;
+    float4* row_out = A.nb + (int64_t)i * KG;
+    auto visit2 = [&](int Tt) -> bool {
+        const TileInfo ti = tile_meta(cl, Tt);
+        float pr[D];
+        const bool need = q.valid && lane_gap2<D>(q, ti, pr) <= tau_hi;
+        if (!__any(need)) return false;
+        stage_f32(cl, ti, L);
+        stage_f64(cl, ti, L);
+        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int j) {
+            const int t = ti.start + j;
+            const bool take = q.valid && key <= tau && t != i;
+            if (take) {
+                if (cnt < KG) {
+                    const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
+                    float v[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int a = 0; a < D; ++a) v[a] = (float)(qq[a] - q.p64[a]);
+                    row_out[cnt] = make_float4(v[0], v[1], v[2], __int_as_float(t));
+                    ++cnt;
+                } else {
+                    over = true;
+                }
+            }
+        });
+        wave_sync();
+        return true;
+    };
+    traverse<D>(cl, q, T, visit2, [&]() { return wave_maxf(q.valid ? tau_hi : -1.f); });
+    if (q.valid) {
+        // r rounded down; an overflowing row (ties at tau beyond kGraphK) certifies nothing
+        const float r = over ? 0.f : __builtin_amdgcn_sqrtf(fmaxf(r2, 0.f)) * 0.99999f;
+        A.nbh[i] = make_float2(r, __int_as_float(cnt));
+    }
+}
+
+// Pack the graph rows into one 128-B line each (GraphArgs / DevCloud::nbq): offsets quantised to
+// int16 in units of s = max |offset| / 32767 (error <= s / 2 per axis, which k_corr's bound adds).
+__global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ nb, const float2* __restrict__ nbh,
+                                                    int64_t n, uint4* __restrict__ nbq, int32_t* __restrict__ nbi) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float2 h = nbh[i];
+    const int cnt = __float_as_int(h.y);
+    float m = 0.f;
+    for (int k = 0; k < cnt; ++k) {
+        const float4 v = nb[i * kGraphK + k];
+        m = fmaxf(m, fmaxf(fabsf(v.x), fmaxf(fabsf(v.y), fabsf(v.z))));
+    }
+    const float s = m > 0.f ? m / 32767.f : 1e-30f;
+    const float inv = 1.f / s;
+    uint32_t w[32];
+    w[0] = __float_as_uint(h.x);
+    w[1] = __float_as_uint(s);
+    int16_t* e = reinterpret_cast<int16_t*>(w + 2);
+    for (int k = 0; k < kGraphK; ++k) {
+        int16_t q[3] = {-32768, 0, 0};
+        int idx = -1;
+        if (k < cnt) {
+            const float4 v = nb[i * kGraphK + k];
+            const float c[3] = {v.x, v.y, v.z};
+            for (int a = 0; a < 3; ++a) q[a] = (int16_t)max(-32767, min(32767, __float2int_rn(c[a] * inv)));
+            idx = __float_as_int(v.w);
+        }
+        for (int a = 0; a < 3; ++a) e[3 * k + a] = q[a];
+        nbi[i * kGraphK + k] = idx;
+    }
+    for (int k = 2 + (3 * kGraphK + 1) / 2; k < 32; ++k) w[k] = 0u;
+    for (int c = 0; c < 8; ++c) nbq[i * 8 + c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+}
+
+// ---------------------------------------------------------------------------
 // per-iteration correspondences + weights + statistics
 // ---------------------------------------------------------------------------
 // Register budget of k_corr: on gfx950 a wave with next_free_sgpr >= 94 leaves 6 waves per SIMD,
@@ -1008,32 +1168,17 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
     }
     for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
-    int pairs = 0, list_rebuilds = 0, namb_total = 0;
+    int pairs = 0, list_rebuilds = 0, namb_total = 0, ngproved = 0, nwalked = 0;
 
     // workgroup -> unit (kCorrWaves consecutive source tiles).  Workgroup b runs on XCD b % 8: the
     // first 8 q8 workgroups are striped so that XCD x walks the contiguous unit range [x q8, x q8 + q8)
-    // (its L2 then holds that region of the target), longest-first within the range by the cost
-    // classes the previous pass recorded; the remaining units run in index order.
+    // in index order (its L2 then holds that region of the target); the remaining units run in index
+    // order.  (Orders that start the previous pass's long units first were measured slower: the
+    // walking set changes from pass to pass)
     const int nunits = (int)gridDim.x, q8 = nunits / 8;
     int unit = (int)blockIdx.x;
-    if (unit < 8 * q8) {
-        const int x = unit & 7, r = unit >> 3;
-        unit = x * q8 + r;
-        if (A.order) {
-            const int par = A.pass & 1;
-            const int32_t* cnt = A.order_cnt + (par * 8 + x) * kOrderBuckets;
-            int tot = 0;
-#pragma unroll
-            for (int k = 0; k < kOrderBuckets; ++k) tot += cnt[k];
-            if (tot == q8) {
-                int rr = r, k = kOrderBuckets - 1;
-                while (k > 0 && rr >= cnt[k]) rr -= cnt[k--];
-                unit = A.order[((int64_t)(par * 8 + x) * kOrderBuckets + k) * q8 + rr];
-            }
-        }
-    }
+    if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
     unit = __builtin_amdgcn_readfirstlane(unit);
-    const unsigned long long wg_t0 = __builtin_amdgcn_s_memtime();
     // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
     int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;
     if (T >= A.q_end) T = -1;
@@ -1116,7 +1261,115 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 cert = cj >= 0 ? 2.f * cdelta < cgap : cgap - cdelta > A.empty_r;
             }
         }
+        // the point relative to its last match jp, fp32 (error well inside the screen margin): the
+        // search cap below and the graph descent start from it
+        bool have_jp = false;
+        float qr[3] = {0.f, 0.f, 0.f}, d2jp = 0.f;
+        if (A.cert_j && q.valid && !cert && jp >= 0 && jp < tg.n) {
+            const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[jp];
+            const double tv[3] = {t4.x, t4.y, t4.z};
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                qr[a] = (float)(q.ow[a] - tv[a]) + q.pw[a];
+                d2jp = fmaf(qr[a], qr[a], d2jp);
+            }
+            have_jp = true;
+        }
+        // ---- graph descent: nearest neighbour proved from the target graph --------
+        // From node j = jp, candidates {j} + row(j).  With b the nearest candidate: any target t nearer
+        // to p' than b lies within d(p', j) + d(p', b) of j (triangle inequality), so if that is < r(j)
+        // t is a candidate and b is the exact nearest; at a local minimum (b = j) the test is
+        // 2 d(p', j) < r(j).  Otherwise hop to b (at most kGraphHops steps) or leave the lane to the
+        // walk.  Distances are fp32 on coordinates relative to the node; e bounds their error.  A near
+        // tie among candidates (gap <= 2e) is left to the walk (its fp64 tie rules).  The lane's new
+        // certificate: every other target is >= min(runner-up, r(j) - d(p', j)) - e away.
+        bool gcert = false;
+        float ggap = 0.f;
+        if (tg.nbq && wave_any(have_jp)) {
+            bool act = have_jp;
+            int node = jp;
+            // error of qr so far (absolute, m): its fp32 formation, then each hop's offset and subtraction
+            float eq = kGraphErr * (st.radius + __builtin_amdgcn_sqrtf(d2jp));
+            for (int h = 0; h < kGraphHops; ++h) {
+                if (!wave_any(act)) break;
+                if (act) {
+                    uint32_t w[32];
+                    const uint4* row = tg.nbq + (int64_t)node * 8;
+                    // the line in two halves (entries 0-8 need dwords 0-15): half the registers live
+                    auto load_half = [&](int c0) {
+#pragma unroll
+                        for (int c = c0; c < c0 + 4; ++c) {
+                            const uint4 v = row[c];
+                            w[4 * c] = v.x;
+                            w[4 * c + 1] = v.y;
+                            w[4 * c + 2] = v.z;
+                            w[4 * c + 3] = v.w;
+                        }
+                    };
+                    load_half(0);
+                    const float r = __uint_as_float(w[0]), sc = __uint_as_float(w[1]);
+                    const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
+                    float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f;
+                    int bk = -1;
+#pragma unroll
+                    for (int k = 0; k < kGraphK; ++k) {
+                        if (k == 9) {
+                            asm volatile("" ::: "memory");   // keep the second half's loads here
+                            load_half(4);
+                        }
+                        int c3[3];
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+                            const int p = 4 + 3 * k + a;   // int16 slot (2 header dwords = 4 slots)
+                            c3[a] = (p & 1) ? ((int)w[p >> 1] >> 16) : (((int)(w[p >> 1] << 16)) >> 16);
+                        }
+                        const float dx = fmaf(-sc, (float)c3[0], qr[0]);
+                        const float dy = fmaf(-sc, (float)c3[1], qr[1]);
+                        const float dz = fmaf(-sc, (float)c3[2], qr[2]);
+                        float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                        dd = c3[0] == -32768 ? 3e38f : dd;   // unused entry
+                        if (dd < b1) {
+                            b2 = b1;
+                            b1 = dd;
+                            bk = k;
+                            bx = dx;
+                            by = dy;
+                            bz = dz;
+                        } else {
+                            b2 = fminf(b2, dd);
+                        }
+                    }
+                    const float d0 = __builtin_amdgcn_sqrtf(d0s);
+                    const float e1 = __builtin_amdgcn_sqrtf(b1), e2 = __builtin_amdgcn_sqrtf(b2);
+                    // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
+                    const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
+                    if (e2 - e1 <= 2.f * e) {
+                        act = false;                              // near tie: the walk decides
+                    } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
+                        gcert = true;
+                        cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
+                        ggap = fminf(e2, r - d0) - e1 - 2.f * e;
+                        act = false;
+                    } else if (bk < 0) {
+                        act = false;                              // local minimum without proof
+                    } else {                                      // hop: p' relative to the nearer candidate
+                        qr[0] = bx;
+                        qr[1] = by;
+                        qr[2] = bz;
+                        eq = e;
+                        node = tg.nbi[(int64_t)node * kGraphK + bk];
+                    }
+                }
+            }
+            if (gcert) {
+                cert = true;
+                cgap = ggap;
+            }
+        }
+        const bool any_gcert = wave_any(gcert);
         const bool skip_walk = !wave_any(q.valid && !cert);
+        ngproved = __popcll(__ballot(gcert));
+        nwalked = skip_walk ? 0 : 1;
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
         // farther than kappa since its last pass (the pose is still converging) walks without it
         const float kap = cdelta > A.kappa ? 0.f : A.kappa;
@@ -1138,19 +1391,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // <= bound_of(b0).  Lanes start the walk at that radius instead of the screen radius; every row
         // within the final bound is still scanned, so the result is unchanged (bit-identical, tested).
         float cap = 3e38f;
-        if (A.cert_j && q.valid && !cert && !skip_walk) {
-            if (jp >= 0 && jp < tg.n) {
-                const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[jp];
-                const double tv[3] = {t4.x, t4.y, t4.z};
-                float d2 = 0.f;
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    const float d = (float)(q.ow[a] - tv[a]) + q.pw[a];
-                    d2 = fmaf(d, d, d2);
-                }
-                cap = bound_of(d2 + 2.f * marg(A.mg, d2)) * 1.0001f;
-            }
-        }
+        if (have_jp && !cert && !skip_walk) cap = bound_of(d2jp + 2.f * marg(A.mg, d2jp)) * 1.0001f;
         // lane search bound: the runner-up, or bound_of(winner), within the cap
         auto lane_bound = [&]() -> float {
             if (!q.valid || cert) return -1.f;
@@ -1222,9 +1463,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             // lane k holds list entry k: its box gap to the wave box, start and count
             int est = 0, ecnt = 0;
             float eg2 = 3e38f;
+            const Query<D> qa = active_box<D>(q, lb >= 0.f);   // the searching lanes' box
             if (l < nl) {
                 ent = A.list[(int64_t)T * kListMax + l];
-                eg2 = gap2_box<D>(q, tg.tiles[ent].c, tg.tiles[ent].h);
+                eg2 = gap2_box<D>(qa, tg.tiles[ent].c, tg.tiles[ent].h);
                 est = tg.tiles[ent].start;
                 ecnt = tg.tiles[ent].count;
             }
@@ -1330,10 +1572,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // that skipped the walk leaves its certificates (and cert_pass) as they are: they stay relative to
         // the older pose, whose direct displacement to later poses is no larger than the summed steps,
         // and the pass writes nothing for it -- until that pose is half the pose ring old.
-        if (A.cert_j && (!skip_walk || A.pass - A.cert_pass[T] >= kPoseRing / 2)) {
+        if (A.cert_j && (!skip_walk || any_gcert || A.pass - A.cert_pass[T] >= kPoseRing / 2)) {
             if (q.valid) {
                 float g = 0.f;
-                if (cert) {
+                if (gcert) {
+                    g = cgap;   // proved at this pass's pose
+                } else if (cert) {
                     g = cj >= 0 ? cgap - 2.f * cdelta : cgap - cdelta;
                 } else if (found) {
                     if (!amb) {   // other targets: scanned >= sec - margin, unscanned > the final bound
@@ -1397,7 +1641,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 return true;
             };
             if (use) {   // the certified candidate list covers every tile within lb >= lim
-                uint64_t em = __ballot(l < nl);
+                const Query<D> qb = active_box<D>(q, amb);   // entries near the re-resolved lanes only
+                bool near = false;
+                const float limw = wave_maxf(amb ? lim : -1.f);
+                if (l < nl) near = gap2_box<D>(qb, tg.tiles[ent].c, tg.tiles[ent].h) <= limw;
+                uint64_t em = __ballot(near);
                 while (em) {
                     const int k = __ffsll((unsigned long long)em) - 1;
                     em &= em - 1;
@@ -1604,6 +1852,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         s_wstat[w][NSS] = (double)namb_total;
         s_wstat[w][NSS + 1] = (double)pairs * 64.0;
         s_wstat[w][NSS + 2] = (double)list_rebuilds;
+        s_wstat[w][NSS + 4] = (double)ngproved;
+        s_wstat[w][NSS + 5] = (double)nwalked;
     }
     S.mark(6);
 #if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
@@ -1637,21 +1887,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         for (int u = 0; u < kCorrWaves; ++u) s += s_wstat[u][t];
         __hip_atomic_store(&A.partials[(int64_t)unit * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (A.order && threadIdx.x == 0 && unit < 8 * q8) {   // cost class of this unit for the next pass
-        const unsigned long long dur = __builtin_amdgcn_s_memtime() - wg_t0 + 1;
-        const int lg2 = 63 - __clzll(dur);
-        const int half = (dur >> (lg2 > 0 ? lg2 - 1 : 0)) & 1;   // sqrt(2) steps
-        const int k = min(kOrderBuckets - 1, max(0, 2 * lg2 + half - 24));
-        const int x = unit / q8, par = (A.pass + 1) & 1;
-        const int pos = atomicAdd(&A.order_cnt[(par * 8 + x) * kOrderBuckets + k], 1);
-        A.order[((int64_t)(par * 8 + x) * kOrderBuckets + k) * q8 + pos] = unit;
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int ng = (int)((gridDim.x + kGroupWG - 1) / kGroupWG);
+    const int ng = (nunits + kGroupWG - 1) / kGroupWG;
     const int g = unit / kGroupWG;   // the reduction follows the unit, not the launch order
     if (threadIdx.x == 0) {
-        const int gn = min(kGroupWG, (int)gridDim.x - g * kGroupWG);
+        const int gn = min(kGroupWG, nunits - g * kGroupWG);
         s_last = __hip_atomic_fetch_add(&A.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
         if (s_last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1724,10 +1965,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     if (!s_last) return;
     sum_rows(A.gpart, 0, ng, s_sum);
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
-    // every workgroup has read this pass's order: its counts become the next pass's append target
-    if (A.order)
-        for (int t = threadIdx.x; t < 8 * kOrderBuckets; t += 64 * kCorrWaves)
-            A.order_cnt[(A.pass & 1) * 8 * kOrderBuckets + t] = 0;
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -2231,6 +2468,16 @@ hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
     else if (dim == 3 && k == 10) hipLaunchKernelGGL((k_knn_cov<3, 10>), dim3(g), dim3(256), 0, st, a);
     else if (dim == 2 && k == 10) hipLaunchKernelGGL((k_knn_cov<2, 10>), dim3(g), dim3(256), 0, st, a);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_graph(const GraphArgs& a, int dim, hipStream_t st) {
+    if (a.cl.ntiles <= 0) return hipSuccess;
+    const unsigned g = (unsigned)((a.cl.ntiles + kWavesPerWG - 1) / kWavesPerWG);
+    if (dim == 2) hipLaunchKernelGGL(k_graph<2>, dim3(g), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_graph<3>, dim3(g), dim3(256), 0, st, a);
+    const unsigned gp = (unsigned)((a.cl.n + 255) / 256);
+    hipLaunchKernelGGL(k_graph_pack, dim3(gp), dim3(256), 0, st, a.nb, a.nbh, a.cl.n, a.nbq, a.nbi);
     return hipGetLastError();
 }
 

@@ -180,6 +180,15 @@ class Engine:
               "gicp_rotated_covariances")
         return out
 
+    def graph(self):
+        """The target neighbour graph (gicp_get_graph): (index [M, 20] original ids with -1 pads,
+        radius [M]: every target nearer than radius[i] to point i is in row i)."""
+        idx = np.empty((self.n_tgt, _lib.GRAPH_K), dtype=np.int64)
+        rad = np.empty(self.n_tgt)
+        check(self._lib.gicp_get_graph(self._ctx, idx.ctypes.data_as(C.POINTER(C.c_int64)), dptr(rad)), self._ctx,
+              "gicp_get_graph")
+        return idx, rad
+
     def reset_cache(self):
         """Forget the pose-dependent caches (lists, certificates, last matches): the next pass starts cold."""
         check(self._lib.gicp_reset_cache(self._ctx), self._ctx, "gicp_reset_cache")
@@ -240,10 +249,12 @@ class Engine:
         return (st, out) if debug else st
 
     def pass_info(self):
-        """Diagnostics of the last pass: ambiguous lanes, pairs screened, list rebuilds, sum |r|^2."""
+        """Diagnostics of the last pass: ambiguous lanes, pairs screened, list rebuilds, sum |r|^2,
+        lanes proved by the graph descent, source tiles that walked."""
         out = np.empty(_lib.PASS_INFO)
         check(self._lib.gicp_pass_info(self._ctx, dptr(out)), self._ctx, "gicp_pass_info")
-        return dict(ambiguous=out[0], pairs=out[1], list_rebuilds=out[2], sum_sq=out[3])
+        return dict(ambiguous=out[0], pairs=out[1], list_rebuilds=out[2], sum_sq=out[3], graph_proved=out[4],
+                    walked_tiles=out[5])
 
     def iterate_top(self, T, k=5):
         """One pass at pose T keeping det(W) on the device, then its top-k on the device

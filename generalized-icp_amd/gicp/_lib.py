@@ -21,7 +21,8 @@ GICP_E_STATE = -3
 GICP_E_COMM = -4
 GICP_E_NOMEM = -5
 COMM_ID_BYTES = 128
-PASS_INFO = 4
+PASS_INFO = 6
+GRAPH_K = 20
 
 # gicp_params.cov_model (include/gicp_hip.h GICP_COV_*)
 COV_MODELS = {"plane_to_plane": 0, "gicp": 0, "point_to_point": 1, "icp": 1, "point_to_plane": 2}
@@ -109,6 +110,7 @@ SIGNATURES = {
     "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
     "gicp_reset_cache": (C.c_int, [_VP]),
+    "gicp_get_graph": (C.c_int, [_VP, C.POINTER(C.c_int64), _DP]),
     "gicp_iteration_times": (C.c_int, [_VP, C.POINTER(C.c_float), C.c_int]),
     "gicp_set_allreduce": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),
     "gicp_rotated_covariances": (C.c_int, [_VP, C.c_int, _DP, _DP]),

@@ -152,6 +152,12 @@ int gicp_target_to_source(gicp_ctx* ctx, int shard, int nshards);
  * original order, [n, dim, dim] (gicp.py:104 target_cov_matrices, :111
  * initial_source_cov_matrices).  which: 0 = target, 1 = source. */
 int gicp_get_covariances(gicp_ctx* ctx, int which, double* out);
+/* The target's neighbour graph (built by gicp_set_target unless GICP_NO_GRAPH=1):
+ * index[M][GICP_GRAPH_K] original indices of up to GICP_GRAPH_K other target points (-1 pads),
+ * radius[M] such that every target within distance < radius[i] of point i is in row i (0: the
+ * row certifies nothing).  Original order.  Either output may be NULL. */
+#define GICP_GRAPH_K 20
+int gicp_get_graph(gicp_ctx* ctx, int64_t* index, double* radius);
 /* Neighbour count (incl. self, < d_n, capped at k) per point, original order. */
 int gicp_get_neighbor_counts(gicp_ctx* ctx, int which, int32_t* out);
 
@@ -165,8 +171,9 @@ int gicp_iterate(gicp_ctx* ctx, const double* T, double* stats, gicp_debug* dbg)
 
 /* Per-pass diagnostics of the last gicp_iterate / gicp_align pass, summed over ranks:
  * out[0] ambiguous lanes re-resolved in fp64, out[1] distance pairs screened, out[2] candidate-list
- * rebuilds, out[3] sum of squared correspondence distances |q - (R s + t)|^2 (PCL's MSE numerator). */
-#define GICP_PASS_INFO 4
+ * rebuilds, out[3] sum of squared correspondence distances |q - (R s + t)|^2 (PCL's MSE numerator),
+ * out[4] points whose nearest target the graph descent proved, out[5] source tiles that walked. */
+#define GICP_PASS_INFO 6
 int gicp_pass_info(gicp_ctx* ctx, double out[GICP_PASS_INFO]);
 
 /* The drop-in's visualisation extras (gicp.py:169-172) without copying per-point arrays: the k

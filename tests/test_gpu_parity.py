@@ -287,15 +287,15 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
     A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
     default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
-    certificates or lists (plain full walks), and one with the longest-first workgroup order, while the
+    certificates or lists (plain full walks), and one without the target graph's descent, while the
     certified passes evaluate far fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1", "plain", "ordered"):
+    for flag in ("0", "1", "plain", "nograph"):
+        monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "nograph" else "0")
         monkeypatch.setenv("GICP_NO_CERTS", "1" if flag in ("1", "plain") else "0")
         monkeypatch.setenv("GICP_NO_LISTS", "1" if flag == "plain" else "0")
-        monkeypatch.setenv("GICP_NO_ORDER", "0" if flag == "ordered" else "1")   # longest-first launch order
         e = gicp.Engine(0)
         try:
             e.set_target(tgt, p)
@@ -311,11 +311,65 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    for other in ("1", "plain", "ordered"):
+    for other in ("1", "plain", "nograph"):
         assert np.array_equal(out["0"][0], out[other][0])
         for a, b in zip(out["0"][1], out[other][1]):
             assert np.array_equal(a, b)
     assert out["0"][3] < 0.05 * out["1"][3]            # the converged pass walked almost nothing
+
+
+def test_target_graph_rows_cover_their_radius(eng, scene3d):
+    """The target neighbour graph: every target nearer than radius[i] to point i is in
+    row i (cKDTree ball query, fp64), rows hold distinct other points, and the radius is the distance
+    of a neighbour the row does not hold (so rows are the nearest ones, up to the screen's error)."""
+    from scipy.spatial import cKDTree
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, **P3)
+    eng.set_target(tgt, p)
+    idx, rad = eng.graph()
+    assert idx.shape == (len(tgt), 20) and np.all(rad > 0)
+    tree = cKDTree(tgt)
+    d21, _ = tree.query(tgt, k=22)
+    assert np.all(rad <= d21[:, 21] * (1 + 1e-5))            # at most the 21st other neighbour's distance
+    # ... and not much below the 20th's, or the neighbourhood cap d_n when fewer lie within it
+    assert np.all(rad >= np.minimum(d21[:, 20], P3["max_distance_nearest_neighbors"]) * (1 - 1e-3) - 1e-6)
+    for i in range(0, len(tgt), 97):
+        row = idx[i][idx[i] >= 0]
+        assert i not in row and len(set(row)) == len(row)
+        ball = [t for t in tree.query_ball_point(tgt[i], rad[i]) if t != i and np.linalg.norm(tgt[t] - tgt[i]) < rad[i]]
+        assert set(ball) <= set(row), i
+
+
+def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
+    """Graph descent proves nearest neighbours while the pose still moves by centimetres to decimetres:
+    a sequence of passes with growing steps gives bit-identical statistics with and without the graph
+    (GICP_NO_GRAPH=1), and with the graph the moving passes screen fewer pairs."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, **P3)
+    poses = []
+    for k, step in enumerate([0.0, 0.002, 0.01, 0.03, 0.08, 0.15, 0.01, 0.001]):
+        T = np.eye(4)
+        T[:3, :3] = S.axis_angle([1.0, 0.5 * k, -0.3], step * 0.2)
+        T[:3, 3] = [step, -0.5 * step, 0.25 * step]
+        poses.append(T)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GICP_NO_GRAPH", flag)
+        e = gicp.Engine(0)
+        try:
+            e.set_target(tgt, p)
+            e.set_source(src, p)
+            sts, pairs = [], []
+            for T in poses:
+                st, dbg = e.iterate(T, debug=True)
+                sts.append((st, dbg["index"]))
+                pairs.append(e.pass_info()["pairs"])
+            out[flag] = (sts, pairs)
+        finally:
+            e.close()
+    for (a, ia), (b, ib) in zip(out["0"][0], out["1"][0]):
+        assert np.array_equal(ia, ib) and np.array_equal(a, b)
+    assert sum(out["0"][1][1:]) < sum(out["1"][1][1:])
 
 
 def test_large_coordinate_offsets(eng):
