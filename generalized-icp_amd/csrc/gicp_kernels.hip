@@ -1136,10 +1136,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     const DevCloud& sc = A.src;
     const DevCloud& tg = A.tgt;
 
-    // pose of this pass from the device state (uniform, scalar loads); converged loops skip
+    // pose of this pass from the device state (uniform, scalar loads); converged loops skip -- tested
+    // once the source tile's metadata is requested too, so both round trips overlap
     typedef __attribute__((address_space(4))) const IterState* ConstState;
     const ConstState cs0 = (ConstState)(uintptr_t)A.state;
-    if (cs0->converged && !A.single_pass) return;
+    const bool done = cs0->converged && !A.single_pass;
     struct {
         double R[9], t[3];
         float R32[9];
@@ -1160,7 +1161,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     if (A.stamps && l == 0)   // stored at once: no register held across the wave
         A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 20 + 16] = __builtin_amdgcn_s_memrealtime();
 #endif
-    if ((A.use_lists || A.cert_j) && blockIdx.x == 0 && threadIdx.x == 0) {   // this pass's pose into the ring
+    if ((A.use_lists || A.cert_j) && blockIdx.x == 0 && threadIdx.x == 0 && !done) {   // this pass's pose into the ring
         double* ring = A.poses + (A.pass % kPoseRing) * 12;
         for (int a = 0; a < 3; ++a) {
             for (int b = 0; b < 3; ++b) ring[a * 3 + b] = (a < D && b < D) ? P.R[a * D + b] : 0.0;
@@ -1182,12 +1183,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
     int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;
     if (T >= A.q_end) T = -1;
+    if (T < 0 && done) return;
     if (T >= 0) {
     bool on = false;          // accepted correspondence
     double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0, r2 = 0.0;
     bool amb = false;
     {
         const TileInfo st = tile_meta(sc, T);
+        if (done) return;
         Query<D> q;
         q.valid = l < st.count;
         const int i = st.start + min(l, st.count - 1);
@@ -1545,9 +1548,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         S.mark(1);
 
-        // the fp64 source point is needed only from here on (kept out of the walk's registers)
-        {
-            const double4 s4 = reinterpret_cast<const double4*>(sc.xyz64)[i];
+        // the fp64 source point is needed only from here on (kept out of the walk's registers).  A wave
+        // that walked needs it now (fp64 fallback); one that skipped the walk requests it with its
+        // matches and covariances in the epilogue: one memory round trip instead of two
+        auto source_point = [&](const double4& s4) {
             const double s4v[3] = {s4.x, s4.y, s4.z};
 #pragma unroll
             for (int a = 0; a < D; ++a) {
@@ -1557,7 +1561,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 q.p64[a] = p;
                 sv[a] = s4v[a];
             }
-        }
+        };
+        if (!skip_walk) source_point(reinterpret_cast<const double4*>(sc.xyz64)[i]);
         const bool found = cert ? cj >= 0 : (q.valid && best < init);
         int j = -1;
         double d2e = 0.0;
@@ -1603,7 +1608,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
 
         // ---- fp64 re-resolution of the lanes the screen could not decide ----
-        if (__any(amb)) {
+        if (!skip_walk && __any(amb)) {
             double bd2 = 1e300;   // exact best d^2 among the rows scanned
             float sd2 = 3e38f;    // runner-up d^2, rounded down (a lower bound is all a certificate needs)
             int bj = -1;   // its sorted index; the original index (tie-break) is read only on exact ties
@@ -1667,11 +1672,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
         S.mark(4);
         // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
+        double4 s4e = make_double4(0.0, 0.0, 0.0, 0.0);
+        if (skip_walk) s4e = reinterpret_cast<const double4*>(sc.xyz64)[i];
         if (found && j >= 0) {
             // match position and both covariances requested together (one memory round trip)
             const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
             const double4 ct = tg.cov[j];
             const double4 cs = sc.cov[i];
+            if (skip_walk) source_point(s4e);
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
             const double dist = sqrt(d2e);
@@ -1743,6 +1751,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = on ? (int64_t)tg.perm[j] : -1;
         } else if (q.valid) {
+            if (skip_walk) source_point(s4e);
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = -1;
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = 1.0 / 0.0;
         }
