@@ -158,6 +158,35 @@ struct Cloud {
     }
 };
 
+// Scratch of one cloud build (grow-only): the synchronous builds and the staged one (which runs on
+// its own stream and host thread while the current target is registered) each own one.
+struct BuildScratch {
+    double* s_in = nullptr;
+    uint32_t *s_codes = nullptr, *s_codes2 = nullptr;
+    int32_t* s_idx = nullptr;
+    unsigned char* s_sort = nullptr;
+    float4* g_nb = nullptr;           // graph build scratch
+    float2* g_nbh = nullptr;
+    int32_t* d_amb = nullptr;         // covariance-kernel diagnostics counter
+    size_t cap_in = 0, cap_codes = 0, cap_codes2 = 0, cap_idx = 0, cap_sort = 0, cap_gnb = 0, cap_gnbh = 0;
+    int cap_k_hint[4] = {0, 0, 0, 0};  // last tile extent-cap step per dimension (tiling warm start)
+    double* h_pinned = nullptr;       // pinned host copy of the input (staged builds)
+    size_t cap_pinned = 0;
+    void release() {
+        dfree(s_in);
+        dfree(s_codes);
+        dfree(s_codes2);
+        dfree(s_idx);
+        dfree(s_sort);
+        dfree(g_nb);
+        dfree(g_nbh);
+        dfree(d_amb);
+        if (h_pinned) (void)hipHostFree(h_pinned);
+        h_pinned = nullptr;
+        cap_in = cap_codes = cap_codes2 = cap_idx = cap_sort = cap_gnb = cap_gnbh = cap_pinned = 0;
+    }
+};
+
 }  // namespace
 
 struct gicp_ctx {
@@ -199,17 +228,20 @@ struct gicp_ctx {
     bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
     bool use_graph = true;            // GICP_NO_GRAPH=1: no target neighbour graph, no graph descent
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
-    // cloud-build scratch and per-source-tile arrays, grow-only (a frame stream allocates once)
-    double* s_in = nullptr;
-    uint32_t *s_codes = nullptr, *s_codes2 = nullptr;
-    int32_t* s_idx = nullptr;
-    unsigned char* s_sort = nullptr;
-    size_t cap_in = 0, cap_codes = 0, cap_codes2 = 0, cap_idx = 0, cap_sort = 0;
+    // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
+    // allocates once)
+    BuildScratch bs;
+    // staged target (gicp_stage_target / gicp_commit_target): built into `next` on stream2 by a host
+    // thread while the current target is registered
+    Cloud next;
+    BuildScratch bs2;
+    hipStream_t stream2 = nullptr;
+    std::thread stager;
+    bool staged = false;
+    int stage_rc = GICP_OK;
+    std::string stage_err;
+    gicp_params pnext{};
     size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0;
-    int cap_k_hint[4] = {0, 0, 0, 0};  // last tile extent-cap step per dimension (tiling warm start)
-    float4* g_nb = nullptr;           // graph build scratch
-    float2* g_nbh = nullptr;
-    size_t cap_gnb = 0, cap_gnbh = 0;
     int pass = 0;
     bool use_lists = true;
     double skin_frac = 0.2;           // candidate-list skin as a fraction of d_c (GICP_SKIN)
@@ -408,8 +440,8 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
 
 // Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
 // is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
-void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p,
-                 bool graph = false) {
+void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
+                 BuildScratch& bs, hipStream_t st, bool pinned_input = false) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -417,7 +449,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     std::string tlog;
     auto tick = [&](const char* what) {
         if (!verbose) return;
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(st));
         const auto t = std::chrono::steady_clock::now();
         char b[64];
         std::snprintf(b, sizeof b, " %s %.1f", what, std::chrono::duration<double, std::milli>(t - tprev).count());
@@ -458,16 +490,21 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
     cl.scale = std::ldexp(1.0, cl.bits) / ext;
     tick("host-scan");
 
-    hipStream_t st = c->stream;
     {
         cl.reserve_points(n);
-        dreserve(c->s_in, c->cap_in, (size_t)n * dim);
-        dreserve(c->s_codes, c->cap_codes, (size_t)n);
-        dreserve(c->s_codes2, c->cap_codes2, (size_t)n);
-        dreserve(c->s_idx, c->cap_idx, (size_t)n);
-        double* d_in = c->s_in;
-        uint32_t *d_codes = c->s_codes, *d_codes_s = c->s_codes2;
-        int32_t* d_idx = c->s_idx;
+        dreserve(bs.s_in, bs.cap_in, (size_t)n * dim);
+        dreserve(bs.s_codes, bs.cap_codes, (size_t)n);
+        dreserve(bs.s_codes2, bs.cap_codes2, (size_t)n);
+        dreserve(bs.s_idx, bs.cap_idx, (size_t)n);
+        if (!bs.d_amb) {
+            dalloc(bs.d_amb, 4);
+            HIPCHK(hipMemsetAsync(bs.d_amb, 0, sizeof(int32_t) * 4, st));
+        }
+        double* d_in = bs.s_in;
+        uint32_t *d_codes = bs.s_codes, *d_codes_s = bs.s_codes2;
+        int32_t* d_idx = bs.s_idx;
+        // (a staged build passes its pinned copy: the H2D copy is then asynchronous)
+        (void)pinned_input;
         HIPCHK(hipMemcpyAsync(d_in, xyz, sizeof(double) * n * dim, hipMemcpyHostToDevice, st));
         DevCloud fr = cl.view();
         HIPCHK(launch_morton(d_in, n, dim, fr, d_codes, d_idx, st));
@@ -475,8 +512,8 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         const unsigned end_bit = (unsigned)(dim * cl.bits);
         HIPCHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0, end_bit,
                                          st));
-        dreserve(c->s_sort, c->cap_sort, tmp_bytes + 16);
-        HIPCHK(rocprim::radix_sort_pairs((void*)c->s_sort, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0,
+        dreserve(bs.s_sort, bs.cap_sort, tmp_bytes + 16);
+        HIPCHK(rocprim::radix_sort_pairs((void*)bs.s_sort, tmp_bytes, d_codes, d_codes_s, d_idx, cl.perm, (size_t)n, 0,
                                          end_bit, st));
         tick("upload+sort");
         std::vector<uint32_t> codes(n);
@@ -485,8 +522,8 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         tick("codes-d2h");
         std::vector<int32_t> tstart, tcount;
         std::vector<uint32_t> tcode;
-        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, c->cap_k_hint[dim & 3]);
-        c->cap_k_hint[dim & 3] = cl.level;
+        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, bs.cap_k_hint[dim & 3]);
+        bs.cap_k_hint[dim & 3] = cl.level;
         tick("tiling");
         cl.ntiles = (int)tstart.size();
         cl.nblocks = (cl.ntiles + kBlockTiles - 1) / kBlockTiles;
@@ -525,7 +562,7 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         ca.min_nb = p.min_neighbors;
         ca.cov_out = cl.cov;
         ca.count_out = cl.ncount;
-        ca.amb_counter = c->d_amb;
+        ca.amb_counter = bs.d_amb;
         HIPCHK(hipMemsetAsync(cl.ncount, 0, sizeof(int32_t) * n, st));
         hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, st);
         if (e == hipErrorInvalidValue) throw Fail{GICP_E_INVALID, "unsupported k_neighbors for this dim (2-D: 6, 10; 3-D: 10, 20)"};
@@ -538,14 +575,14 @@ void build_cloud(gicp_ctx* c, Cloud& cl, const double* xyz, int64_t n, int dim, 
         if (graph) {   // target neighbour graph for k_corr's graph descent
             dreserve(cl.nbq, cl.cap_nbq, (size_t)n * 8);
             dreserve(cl.nbi, cl.cap_nbi, (size_t)n * kGraphK);
-            dreserve(c->g_nb, c->cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
-            dreserve(c->g_nbh, c->cap_gnbh, (size_t)n);
+            dreserve(bs.g_nb, bs.cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
+            dreserve(bs.g_nbh, bs.cap_gnbh, (size_t)n);
             GraphArgs ga{};
             ga.cl = cl.view();
             ga.mg = ca.mg;
             ga.search2 = ca.search2;
-            ga.nb = c->g_nb;
-            ga.nbh = c->g_nbh;
+            ga.nb = bs.g_nb;
+            ga.nbh = bs.g_nbh;
             ga.nbq = cl.nbq;
             ga.nbi = cl.nbi;
             HIPCHK(launch_graph(ga, dim, st));
@@ -863,9 +900,7 @@ int gicp_create(gicp_ctx** out, int device) {
     }
     const int rc = guard_impl(c, "gicp_create", [&] {
         HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        dalloc(c->d_amb, 4);
         for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-        HIPCHK(hipMemsetAsync(c->d_amb, 0, sizeof(int32_t) * 4, c->stream));
     });
     if (rc != GICP_OK) {
         gicp_destroy(c);
@@ -877,6 +912,7 @@ int gicp_create(gicp_ctx** out, int device) {
 
 void gicp_destroy(gicp_ctx* c) {
     if (!c) return;
+    if (c->stager.joinable()) c->stager.join();   // a staged build still running
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -887,7 +923,6 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_state);
     dfree(c->d_tickets);
     dfree(c->d_gpart);
-    dfree(c->d_amb);
     dfree(c->d_dbg_idx);
     dfree(c->d_dbg_w);
     dfree(c->d_dbg_dist);
@@ -903,13 +938,10 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_list_pass);
     dfree(c->d_list_rcert);
     dfree(c->d_poses);
-    dfree(c->s_in);
-    dfree(c->s_codes);
-    dfree(c->s_codes2);
-    dfree(c->s_idx);
-    dfree(c->s_sort);
-    dfree(c->g_nb);
-    dfree(c->g_nbh);
+    c->bs.release();
+    c->bs2.release();
+    c->next.release();
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_xchg) (void)hipHostFree(c->h_xchg);
     dfree(c->d_rot);
@@ -954,7 +986,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c, c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs);
+        build_cloud(c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs, c->bs, c->stream);
         if (c->src.n) reset_tile_state(c);
     });
 }
@@ -966,7 +998,7 @@ int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gi
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         c->psrc = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c, c->src, xyz, N, dim, c->psrc);
+        build_cloud(c->src, xyz, N, dim, c->psrc, false, c->bs, c->stream);
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
     });
@@ -1206,6 +1238,78 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             *res = r;
         }
     });
+}
+
+int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_stage_target", [&] {
+        if (c->staged) throw Fail{GICP_E_STATE, "a staged target is pending (gicp_commit_target or gicp_cancel_stage first)"};
+        if (!xyz || M <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
+        c->pnext = resolve(dim, p);
+        if (!c->stream2) HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        const size_t need = (size_t)M * dim;
+        if (need > c->bs2.cap_pinned) {   // grow-only pinned staging buffer (allocated here, not in the worker)
+            if (c->bs2.h_pinned) HIPCHK(hipHostFree(c->bs2.h_pinned));
+            c->bs2.h_pinned = nullptr;
+            c->bs2.cap_pinned = 0;
+            const size_t cap = need + need / 8;
+            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->bs2.h_pinned), sizeof(double) * cap));
+            c->bs2.cap_pinned = cap;
+        }
+        c->staged = true;
+        c->stage_rc = GICP_OK;
+        c->stage_err.clear();
+        const bool graph = c->use_graph && c->use_certs;
+        const int dev = c->device;
+        c->stager = std::thread([c, xyz, M, dim, graph, dev] {
+            try {
+                HIPCHK(hipSetDevice(dev));
+                std::memcpy(c->bs2.h_pinned, xyz, sizeof(double) * (size_t)M * dim);
+                build_cloud(c->next, c->bs2.h_pinned, M, dim, c->pnext, graph, c->bs2, c->stream2, true);
+            } catch (const Fail& f) {
+                c->stage_rc = f.code;
+                c->stage_err = f.msg;
+            } catch (const std::bad_alloc&) {
+                c->stage_rc = GICP_E_NOMEM;
+                c->stage_err = "out of host memory";
+            } catch (...) {
+                c->stage_rc = GICP_E_INVALID;
+                c->stage_err = "unknown error";
+            }
+        });
+    });
+}
+
+int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_commit_target", [&] {
+        if (!c->staged) throw Fail{GICP_E_STATE, "no staged target (gicp_stage_target first)"};
+        if (c->stager.joinable()) c->stager.join();
+        c->staged = false;
+        if (c->stage_rc != GICP_OK) throw Fail{c->stage_rc, "staged build: " + c->stage_err};
+        if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
+        // the current target (index + covariances) becomes the source, as robot-visualization.py:250
+        // swaps scans, and the staged cloud the target; the old source's buffers wait in `next`
+        if (c->tgt.n) {
+            std::swap(c->src, c->tgt);
+            c->psrc = c->ptgt;
+        }
+        std::swap(c->tgt, c->next);
+        c->next.n = 0;
+        c->next.cov_ready = false;
+        c->next.graph_ready = false;
+        c->ptgt = c->pnext;
+        c->top_ready = false;
+        if (c->src.n) set_shard(c, shard, nshards);
+        HIPCHK(hipStreamSynchronize(c->stream));
+    });
+}
+
+int gicp_cancel_stage(gicp_ctx* c) {
+    if (!c) return GICP_E_INVALID;
+    if (c->stager.joinable()) c->stager.join();
+    c->staged = false;
+    return GICP_OK;
 }
 
 int gicp_reset_cache(gicp_ctx* c) {

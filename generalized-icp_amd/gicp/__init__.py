@@ -111,6 +111,7 @@ class Engine:
         self.dim = None
         self.n_src = self.n_tgt = 0
         self.generation = 0        # bumped whenever the source cloud changes (lazy covariance views)
+        self._staged = None        # (array, params) of a staged target: kept alive until committed
         self._hook = None          # keeps the ctypes callback of set_allreduce alive
 
     def close(self):
@@ -160,6 +161,28 @@ class Engine:
         self.n_src = self.n_tgt
         self.n_tgt = 0
         self.generation += 1
+
+    def stage_target(self, pts, params=None):
+        """Build `pts` as the NEXT target on a second stream while the current one is registered
+        (gicp_stage_target); gicp_commit_target (commit_target) makes it current."""
+        a = self._cloud(pts)
+        p = params or default_params(a.shape[1])
+        check(self._lib.gicp_stage_target(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p)), self._ctx,
+              "gicp_stage_target")
+        self._staged = (a, p)
+
+    def commit_target(self, shard=0, nshards=1):
+        """Wait for the staged target; the current target becomes the source, the staged one the target."""
+        staged, self._staged = self._staged, None
+        check(self._lib.gicp_commit_target(self._ctx, shard, nshards), self._ctx, "gicp_commit_target")
+        if self.n_tgt:
+            self.n_src = self.n_tgt
+            self.generation += 1
+        self.n_tgt, self.dim = staged[0].shape
+
+    def cancel_stage(self):
+        self._lib.gicp_cancel_stage(self._ctx)
+        self._staged = None
 
     def covariances(self, which="target"):
         w = 0 if which == "target" else 1

@@ -110,6 +110,9 @@ SIGNATURES = {
     "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
     "gicp_reset_cache": (C.c_int, [_VP]),
+    "gicp_stage_target": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params)]),
+    "gicp_commit_target": (C.c_int, [_VP, C.c_int, C.c_int]),
+    "gicp_cancel_stage": (C.c_int, [_VP]),
     "gicp_get_graph": (C.c_int, [_VP, C.POINTER(C.c_int64), _DP]),
     "gicp_iteration_times": (C.c_int, [_VP, C.POINTER(C.c_float), C.c_int]),
     "gicp_set_allreduce": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),

@@ -3,7 +3,11 @@
 
 Each new scan becomes the target; the previous target, with its index and covariances already on
 the GPU, becomes the source (`gicp_target_to_source`, robot-visualization.py:250) — so per frame
-only the new scan is uploaded, sorted, tiled and given covariances.  `gicp(prev, cur)` maps the
+only the new scan is uploaded, sorted, tiled and given covariances.  Given the next scan
+(`step(scan, next_scan)` / `run(scans)`), that build runs on a second stream from a host thread
+while the current pair is registered (`gicp_stage_target` / `gicp_commit_target`), so setup leaves
+the critical path (the demo likewise prepares the next scan while its worker registers,
+robot-visualization.py:239-252).  `gicp(prev, cur)` maps the
 previous sensor frame into the current one (p_cur = T p_prev), so the sensor pose advances by
 T^-1: `composition='se3'` (default) is that exact SE(d) update; `composition='reference'` is the
 demo's first-order update (robot-visualization.py:257-265: translation -T[:2, d], yaw
@@ -38,16 +42,31 @@ class Odometry:
         self.yaw_xy = (0.0, 0.0, 0.0)        # reference-formula state (x, y, yaw)
         self.last_T = None
         self.frames = 0
+        if getattr(self, "_staged", None) is not None:
+            self.eng.cancel_stage()
+        self._staged = None                  # the scan object whose build is staged
         self.timing = {"setup_s": 0.0, "align_s": 0.0, "iterations": 0}
 
-    def step(self, scan):
+    def _prep(self, scan):
+        return np.ascontiguousarray(np.asarray(scan, dtype=np.float64)[:, :self.dim])
+
+    def step(self, scan, next_scan=None):
         """Add one scan; returns (T, result) of its registration against the previous scan, or
-        (None, None) for the first frame."""
-        scan = np.ascontiguousarray(np.asarray(scan, dtype=np.float64)[:, :self.dim])
+        (None, None) for the first frame.  `next_scan`, if given, is built on the device while this
+        pair is registered; pass the same object as `scan` of the next call."""
         t0 = time.perf_counter()
-        if self.frames > 0:
-            self.eng.target_to_source()
-        self.eng.set_target(scan, self.params)
+        if self._staged is not None and self._staged is scan:
+            self.eng.commit_target()            # built during the last registration
+        else:
+            if self._staged is not None:
+                self.eng.cancel_stage()
+            if self.frames > 0:
+                self.eng.target_to_source()
+            self.eng.set_target(self._prep(scan), self.params)
+        self._staged = None
+        if next_scan is not None:
+            self.eng.stage_target(self._prep(next_scan), self.params)
+            self._staged = next_scan
         t1 = time.perf_counter()
         self.timing["setup_s"] += t1 - t0
         self.frames += 1
@@ -60,6 +79,16 @@ class Odometry:
         self.last_T = T
         self._integrate(T)
         return T, res
+
+    def run(self, scans):
+        """Register a whole stream (each scan's build overlapped with the previous registration);
+        yields (T, result) per scan."""
+        it = iter(scans)
+        cur = next(it, None)
+        while cur is not None:
+            nxt = next(it, None)
+            yield self.step(cur, nxt)
+            cur = nxt
 
     def _integrate(self, T):
         self.pose, self.yaw_xy = compose(self.pose, T, self.composition, self.yaw_xy)

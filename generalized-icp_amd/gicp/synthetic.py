@@ -322,18 +322,23 @@ def lidar_scene(radius=14.0, clearance=2.5, seed=42):
     return Scene3D(rects, np.asarray(sph).reshape(-1, 4))
 
 
-def lidar_trajectory(frames, seed=7, radius=14.0, step=0.15, yaw_step_deg=0.5, height=1.8):
-    """Sensor-to-world poses (4x4) along a circle of `radius`: per frame ~`step` m and ~`yaw_step_deg`
-    of yaw (jittered by rng(seed)), the sensor looking along the path."""
+def lidar_trajectory(frames, seed=7, radius=14.0, step=0.5, yaw_step_deg=0.5, height=1.8, along_path=False):
+    """Sensor-to-world poses (4x4) on a circle of `radius`: per frame ~`step` m
+    along the circle and ~`yaw_step_deg` of yaw, both jittered by +-10 % from rng(seed).  A 0.5 m /
+    0.5 deg frame cannot follow a circle that fits the 40 m room (0.5 deg per 0.5 m is a 57 m
+    radius), so the sensor's yaw turns at its own rate; `along_path=True` instead keeps it looking
+    along the path (yaw step = step / radius)."""
     rng = np.random.default_rng(seed)
     poses = []
-    ang = 0.0
+    ang, yaw = 0.0, math.pi / 2
     for _ in range(frames):
         T = np.eye(4)
-        T[:3, :3] = axis_angle((0, 0, 1), ang + math.pi / 2)
+        T[:3, :3] = axis_angle((0, 0, 1), ang + math.pi / 2 if along_path else yaw)
         T[:3, 3] = (radius * math.cos(ang), radius * math.sin(ang), height)
         poses.append(T)
         ang += step / radius * (1.0 + 0.2 * (rng.random() - 0.5))
+        if not along_path:
+            yaw += math.radians(yaw_step_deg) * (1.0 + 0.2 * (rng.random() - 0.5))
     return np.asarray(poses)
 
 
@@ -410,10 +415,11 @@ def _lidar_scan_torch(torch, scene, pose, dirs, rng, max_range, noise, device):
     return dirs[hit] * rng_[:, None]
 
 
-def lidar_stream(frames, beams=64, azimuths=1563, seed=7, xp=None, device=None):
-    """Generator of (scan_k, pose_k) for k = 0..frames-1 (scans in sensor coordinates)."""
+def lidar_stream(frames, beams=64, azimuths=1563, seed=7, xp=None, device=None, **traj):
+    """Generator of (scan_k, pose_k) for k = 0..frames-1 (scans in sensor coordinates); `traj`:
+    lidar_trajectory keywords (step, yaw_step_deg, along_path)."""
     scene = lidar_scene()
-    poses = lidar_trajectory(frames, seed=seed)
+    poses = lidar_trajectory(frames, seed=seed, **traj)
     dirs = lidar_dirs(beams, azimuths)
     rng = np.random.default_rng(seed + 1)
     for k in range(frames):

@@ -148,6 +148,16 @@ int gicp_set_source(gicp_ctx* ctx, const double* xyz, int64_t N, int dim, const 
  * as robot-visualization.py:250 swaps scans; then set a new target. */
 int gicp_target_to_source(gicp_ctx* ctx, int shard, int nshards);
 
+/* Double-buffered frame stream (robot-visualization.py:239-252): build the
+ * NEXT target -- pinned copy, upload, Morton sort, tiling, covariances, neighbour graph -- on a
+ * second stream from a host thread while the current target is registered (gicp_align on the
+ * first stream runs concurrently).  `xyz` must stay valid until gicp_commit_target returns.
+ * gicp_commit_target waits for the build, then promotes: current target -> source (as
+ * gicp_target_to_source), staged cloud -> target.  gicp_cancel_stage waits and drops it. */
+int gicp_stage_target(gicp_ctx* ctx, const double* xyz, int64_t M, int dim, const gicp_params* p);
+int gicp_commit_target(gicp_ctx* ctx, int shard, int nshards);
+int gicp_cancel_stage(gicp_ctx* ctx);
+
 /* Surface covariances C = a I - m m^T of the last set_target/set_source,
  * original order, [n, dim, dim] (gicp.py:104 target_cov_matrices, :111
  * initial_source_cov_matrices).  which: 0 = target, 1 = source. */

@@ -58,12 +58,41 @@ def test_lidar_scan_hits_and_noise():
     assert np.max(d_best) < 1e-9
 
 
+def test_trajectory_follows_the_c5_spec():
+    """~0.5 m and ~0.5 deg of yaw per frame (+-10 % jitter)."""
+    P = S.lidar_trajectory(200)
+    for k in range(1, 200):
+        d = np.linalg.inv(P[k - 1]) @ P[k]
+        assert 0.44 < np.linalg.norm(d[:3, 3]) < 0.56
+        assert math.radians(0.44) < S.rotation_angle_error(d, np.eye(4)) < math.radians(0.56)
+
+
+@pytest.mark.gpu
+def test_staged_stream_equals_synchronous_stream():
+    """The double-buffered stream (next scan built on a second stream during the registration,
+    gicp_stage_target / gicp_commit_target) gives bit-identical registrations to building each scan
+    when it is needed, on the C5 trajectory (0.5 m / 0.5 deg frames, constant-velocity start)."""
+    import gicp
+    from gicp.odometry import Odometry
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    frames = [f for f, _ in S.lidar_stream(6, beams=32, azimuths=900)]
+    out = {}
+    for mode in ("sync", "staged"):
+        odo = Odometry(3, params=gicp.default_params(3, max_iterations=30, tolerance=1e-9, **kw))
+        Ts = [odo.step(f)[0] for f in frames] if mode == "sync" else [T for T, _ in odo.run(frames)]
+        out[mode] = (Ts, odo.pose.copy())
+        odo.eng.close()
+    for a, b in zip(out["sync"][0][1:], out["staged"][0][1:]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(out["sync"][1], out["staged"][1])
+
+
 @pytest.mark.gpu
 def test_odometry_stream_vs_oracle_and_truth():
     from oracle import gicp_oracle as O
     from gicp.odometry import Odometry
     kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
-    frames = list(S.lidar_stream(4, beams=16, azimuths=600))
+    frames = list(S.lidar_stream(4, beams=16, azimuths=600, step=0.15, along_path=True))
     import gicp
     odo = Odometry(3, params=gicp.default_params(3, max_iterations=40, tolerance=1e-10, **kw), init="identity")
     pose_oracle = np.eye(4)
