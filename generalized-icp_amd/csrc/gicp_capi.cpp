@@ -8,6 +8,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstddef>
@@ -79,6 +82,72 @@ void dreserve(T*& p, size_t& cap, size_t n) {
     dalloc(p, want);
     cap = want;
 }
+
+// A few persistent host threads for the tiling (spawning threads per cloud costs tens of us each,
+// which a 100k-point frame of a stream cannot afford).  run(n, fn) calls fn(0 .. n-1) on the workers
+// and the calling thread and returns when all are done; one caller at a time.
+class WorkerPool {
+public:
+    explicit WorkerPool(int workers) {
+        for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int tasks, std::function<void(int)> fn) {
+        std::unique_lock<std::mutex> lk(m_);
+        job_ = std::move(fn);
+        ntasks_ = tasks;
+        next_ = done_ = 0;
+        ++gen_;
+        lk.unlock();
+        cv_.notify_all();
+        work();
+        lk.lock();
+        done_cv_.wait(lk, [&] { return done_ == ntasks_ && active_ == 0; });
+    }
+
+private:
+    void work() {
+        for (;;) {
+            int k;
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (next_ >= ntasks_) return;
+                k = next_++;
+            }
+            job_(k);
+            std::lock_guard<std::mutex> g(m_);
+            if (++done_ == ntasks_) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(m_);
+        long seen = 0;
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            ++active_;
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--active_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(int)> job_;
+    int ntasks_ = 0, next_ = 0, done_ = 0, active_ = 0;
+    long gen_ = 0;
+    bool stop_ = false;
+};
 
 // One indexed cloud on the device.
 struct Cloud {
@@ -172,6 +241,16 @@ struct BuildScratch {
     int cap_k_hint[4] = {0, 0, 0, 0};  // last tile extent-cap step per dimension (tiling warm start)
     double* h_pinned = nullptr;       // pinned host copy of the input (staged builds)
     size_t cap_pinned = 0;
+    std::unique_ptr<WorkerPool> pool;  // tiling threads (lazily started)
+    hipStream_t side = nullptr;       // graph build, concurrent with the covariances
+    hipEvent_t ev = nullptr;
+    WorkerPool& workers() {
+        if (!pool) {
+            const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+            pool.reset(new WorkerPool((int)std::min(7u, hc > 1 ? hc - 1 : 0u)));
+        }
+        return *pool;
+    }
     void release() {
         dfree(s_in);
         dfree(s_codes);
@@ -183,6 +262,11 @@ struct BuildScratch {
         dfree(d_amb);
         if (h_pinned) (void)hipHostFree(h_pinned);
         h_pinned = nullptr;
+        pool.reset();
+        if (side) (void)hipStreamDestroy(side);
+        if (ev) (void)hipEventDestroy(ev);
+        side = nullptr;
+        ev = nullptr;
         cap_in = cap_codes = cap_codes2 = cap_idx = cap_sort = cap_gnb = cap_gnbh = cap_pinned = 0;
     }
 };
@@ -312,7 +396,8 @@ float screen_bound(const Margin& m, double d) {
 // tile count stays <= 1.35x the minimum ceil(n/64): tiles are as compact as that budget allows, and
 // the cap bounds the largest tile, which sets both the widest query wave and the loosest box.
 void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
-                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out, int k_hint) {
+                      std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out, int k_hint,
+                      WorkerPool& pool) {
     const int64_t n = (int64_t)codes.size();
     static const double budget = [] {   // GICP_TILE_BUDGET: tile-count budget over ceil(n / 64)
         const char* e = std::getenv("GICP_TILE_BUDGET");
@@ -338,11 +423,14 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
         return x;
     };
     std::vector<uint16_t> g((size_t)n * dim);
-    for (int64_t i = 0; i < n; ++i) {
-        const uint32_t c = codes[i];
-        for (int a = 0; a < dim; ++a)
-            g[(size_t)i * dim + a] = (uint16_t)(dim == 3 ? compact3(c >> a) : compact2(c >> a));
-    }
+    constexpr int kSeg = 16;   // fixed segments (independent of the host's core count: deterministic)
+    pool.run(kSeg, [&](int k) {
+        for (int64_t i = n * k / kSeg; i < n * (k + 1) / kSeg; ++i) {
+            const uint32_t c = codes[i];
+            for (int a = 0; a < dim; ++a)
+                g[(size_t)i * dim + a] = (uint16_t)(dim == 3 ? compact3(c >> a) : compact2(c >> a));
+        }
+    });
     // greedy cut of points [b, e) (a forced break at b); appends (start, count) pairs if `out`
     auto cut_seg = [&](int64_t b, int64_t e, int E, std::vector<int32_t>* out) -> int64_t {
         int64_t nt = 0, i0 = b;
@@ -376,24 +464,14 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
         }
         return nt;
     };
-    // 16 fixed segments (independent of the host's core count, so the tiling is deterministic),
-    // cut concurrently
-    constexpr int kSeg = 16;
+    // the 16 segments are cut concurrently on the pool
     std::vector<std::vector<int32_t>> seg_out(kSeg);
     auto cut = [&](int E, bool emit) -> int64_t {
         int64_t nt_seg[kSeg] = {};
-        auto work = [&](int s0, int s1) {
-            for (int k = s0; k < s1; ++k) {
-                if (emit) seg_out[k].clear();
-                nt_seg[k] = cut_seg(n * k / kSeg, n * (k + 1) / kSeg, E, emit ? &seg_out[k] : nullptr);
-            }
-        };
-        // threads only pay off past a few hundred thousand points (spawn cost ~ tens of us each)
-        const int nth = n < 400000 ? 1 : (int)std::max(1u, std::min<unsigned>(kSeg, std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        for (int t = 1; t < nth; ++t) th.emplace_back(work, kSeg * t / nth, kSeg * (t + 1) / nth);
-        work(0, kSeg / nth);
-        for (auto& x : th) x.join();
+        pool.run(kSeg, [&](int k) {
+            if (emit) seg_out[k].clear();
+            nt_seg[k] = cut_seg(n * k / kSeg, n * (k + 1) / kSeg, E, emit ? &seg_out[k] : nullptr);
+        });
         int64_t nt = 0;
         for (int k = 0; k < kSeg; ++k) nt += nt_seg[k];
         if (emit)
@@ -522,7 +600,7 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         tick("codes-d2h");
         std::vector<int32_t> tstart, tcount;
         std::vector<uint32_t> tcode;
-        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, bs.cap_k_hint[dim & 3]);
+        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, bs.cap_k_hint[dim & 3], bs.workers());
         bs.cap_k_hint[dim & 3] = cl.level;
         tick("tiling");
         cl.ntiles = (int)tstart.size();
@@ -563,16 +641,16 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         ca.cov_out = cl.cov;
         ca.count_out = cl.ncount;
         ca.amb_counter = bs.d_amb;
-        HIPCHK(hipMemsetAsync(cl.ncount, 0, sizeof(int32_t) * n, st));
-        hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, st);
-        if (e == hipErrorInvalidValue) throw Fail{GICP_E_INVALID, "unsupported k_neighbors for this dim (2-D: 6, 10; 3-D: 10, 20)"};
-        HIPCHK(e);
-        HIPCHK(hipStreamSynchronize(st));
-        cl.cov_ready = true;
-        cl.cov_q_begin = qb;
-        cl.cov_q_end = qe;
-        tick("covariances");
-        if (graph) {   // target neighbour graph for k_corr's graph descent
+        // the target neighbour graph (k_corr's graph descent) walks the same cloud as the
+        // covariances but writes other arrays: it runs concurrently on a side stream (each kernel alone
+        // fills only part of the GPU at stream-frame sizes)
+        hipStream_t side = nullptr;
+        if (graph) {
+            if (!bs.side) {
+                HIPCHK(hipStreamCreateWithFlags(&bs.side, hipStreamNonBlocking));
+                HIPCHK(hipEventCreateWithFlags(&bs.ev, hipEventDisableTiming));
+            }
+            side = bs.side;
             dreserve(cl.nbq, cl.cap_nbq, (size_t)n * 8);
             dreserve(cl.nbi, cl.cap_nbi, (size_t)n * kGraphK);
             dreserve(bs.g_nb, bs.cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
@@ -585,8 +663,21 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
             ga.nbh = bs.g_nbh;
             ga.nbq = cl.nbq;
             ga.nbi = cl.nbi;
-            HIPCHK(launch_graph(ga, dim, st));
-            HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipEventRecord(bs.ev, st));
+            HIPCHK(hipStreamWaitEvent(side, bs.ev, 0));
+            HIPCHK(launch_graph(ga, dim, side));
+        }
+        HIPCHK(hipMemsetAsync(cl.ncount, 0, sizeof(int32_t) * n, st));
+        hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, st);
+        if (e == hipErrorInvalidValue) throw Fail{GICP_E_INVALID, "unsupported k_neighbors for this dim (2-D: 6, 10; 3-D: 10, 20)"};
+        HIPCHK(e);
+        HIPCHK(hipStreamSynchronize(st));
+        cl.cov_ready = true;
+        cl.cov_q_begin = qb;
+        cl.cov_q_end = qe;
+        tick("covariances");
+        if (side) {
+            HIPCHK(hipStreamSynchronize(side));
             cl.graph_ready = true;
             tick("graph");
         }
@@ -1179,7 +1270,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             // a host exchange synchronises every iteration anyway: batches of one, so the loop stops
             // at the converged iteration without launching more
             const int B = std::min(prm.max_iterations - enq,
-                                   c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 4);
+                                   c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 8);
             for (int b = 0; b < B; ++b) {
                 CorrArgs a = corr_args(c, 0);
                 const bool ev = timing && (enq + b) % kEvStride == kEvOffset;
