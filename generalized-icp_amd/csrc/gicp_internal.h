@@ -35,7 +35,10 @@ constexpr int kSub = GICP_SUB_TILES;
 constexpr int kSubRows = 64 / kSub;    // rows per sub-tile (a multiple of 4: the scan's row group)
 // target neighbour graph: each target point's kGraphK nearest other target points
 constexpr int kGraphK = 20;
-constexpr int kGraphHops = 4;      // descent steps a k_corr lane may take before it walks
+#ifndef GICP_GRAPH_HOPS
+#define GICP_GRAPH_HOPS 4
+#endif
+constexpr int kGraphHops = GICP_GRAPH_HOPS;   // descent steps a k_corr lane may take before it walks
 // error bound of the descent's fp32 distances, per metre of the coordinates involved (2^-19: the
 // relative-to-node arithmetic errs by a few 2^-24 per operation)
 constexpr float kGraphErr = 1.9073486328125e-06f;

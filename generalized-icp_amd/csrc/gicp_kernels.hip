@@ -1291,6 +1291,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (tg.nbq && wave_any(have_jp)) {
             bool act = have_jp;
             int node = jp;
+            bool tie = false;       // a near tie the row covers: resolved in fp64 below
+            int tnode = 0;
+            float tfar = 0.f;
             // error of qr so far (absolute, m): its fp32 formation, then each hop's offset and subtraction
             float eq = kGraphErr * (st.radius + __builtin_amdgcn_sqrtf(d2jp));
             for (int h = 0; h < kGraphHops; ++h) {
@@ -1347,7 +1350,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
                     const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
                     if (e2 - e1 <= 2.f * e) {
-                        act = false;                              // near tie: the walk decides
+                        // near tie: if the row covers it (same test as below), the nearest is one of the
+                        // candidates within e1 + 2e, resolved exactly after the loop
+                        tie = d0 + e1 + 2.f * e < r;
+                        tfar = r - d0 - e;   // every target outside the row is at least this far
+                        tnode = node;
+                        act = false;                              // else the walk decides
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
@@ -1362,6 +1370,51 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         eq = e;
                         node = tg.nbi[(int64_t)node * kGraphK + bk];
                     }
+                }
+            }
+            // near ties: every candidate of the tie node's row (and the node) exactly in fp64, the nearest
+            // by the KD-tree's tie rule (smaller original index); the lane's certificate gap is the exact
+            // runner-up among them, or the row's reach when that is nearer
+            if (wave_any(tie)) {
+                if (tie) {
+                    double p64[D];
+                    {
+                        const double4 s4 = reinterpret_cast<const double4*>(A.src.xyz64)[i];
+                        const double s4v[3] = {s4.x, s4.y, s4.z};
+#pragma unroll
+                        for (int a = 0; a < D; ++a) {
+                            double p = P.t[a];
+#pragma unroll
+                            for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
+                            p64[a] = p;
+                        }
+                    }
+                    double bd2 = 1e300, sd2 = 1e300;
+                    int bj = -1, bo = 0x7fffffff;
+                    auto consider = [&](int t) {
+                        const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[t];
+                        const double tv[3] = {t4.x, t4.y, t4.z};
+                        const double d2 = dist2_exact<D>(tv, p64);
+                        const int og = tg.perm[t];
+                        if (d2 < bd2 || (d2 == bd2 && og < bo)) {
+                            sd2 = bd2;
+                            bd2 = d2;
+                            bj = t;
+                            bo = og;
+                        } else {
+                            sd2 = fmin(sd2, d2);
+                        }
+                    };
+                    consider(tnode);
+                    const int32_t* ri = tg.nbi + (int64_t)tnode * kGraphK;
+                    for (int k = 0; k < kGraphK; ++k) {
+                        const int t = ri[k];
+                        if (t >= 0) consider(t);
+                    }
+                    gcert = bj >= 0;
+                    cj = bj;
+                    const double g = (fmin(sqrt(sd2), (double)tfar) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
+                    ggap = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
                 }
             }
             if (gcert) {
