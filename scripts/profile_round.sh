@@ -1,10 +1,12 @@
 #!/bin/bash
-# Round profile of the default bench command: kernel-trace stats, per-iteration trace, PMC
-# passes (instruction mix, waits) and the HBM-side traffic summary.  Output: gpurun_out/$1/.
+# Round profile of the default bench command: kernel-trace stats, per-iteration trace, PMC passes
+# (instruction mix, waits) and the HBM-side traffic summary; then the bench line (which reads the
+# traffic just measured).  Usage: scripts/profile_round.sh OUTNAME PROFILEDIR   (e.g. r02 profiles/r02)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
-mkdir -p $OUT
+PD=${2:-profiles/r02}
+mkdir -p $OUT $PD
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o t --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/trace.err || { echo trace failed; exit 1; }
 python3 scripts/trace_iters.py $OUT/trace 30 > $OUT/iterations.txt
 i=0
@@ -17,7 +19,8 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_I
 done
 python3 scripts/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt
 python3 scripts/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json k_corr 3d_room_1000k_1000k_k20
-# the bench line last: its roofline.traffic reads the pmc_traffic.json written above (copied to profiles/)
-cp $OUT/pmc_traffic.json profiles/r01/pmc_traffic.json
+cp $OUT/pmc_traffic.json $PD/pmc_traffic.json
 timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
+cp $OUT/bench.json $PD/bench.json; cp $OUT/iterations.txt $PD/iterations.txt; cp $OUT/pmc_summary.txt $PD/pmc_summary.txt
+cp $OUT/trace/t_kernel_stats.csv $PD/kernel_stats.csv; cp $OUT/bench_under_rocprof.json $PD/bench_under_rocprof.json
 echo done
