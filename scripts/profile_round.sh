@@ -19,8 +19,8 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_I
 done
 python3 scripts/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt
 python3 scripts/pmc_traffic.py $OUT/pmc $OUT/pmc_traffic.json k_corr 3d_room_1000k_1000k_k20
-cp $OUT/pmc_traffic.json $PD/pmc_traffic.json
+cp $OUT/pmc_traffic.json $PD/pmc_traffic.json   # (on the box: read by the bench line below; gpurun_out/ is what comes back)
 timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
-cp $OUT/bench.json $PD/bench.json; cp $OUT/iterations.txt $PD/iterations.txt; cp $OUT/pmc_summary.txt $PD/pmc_summary.txt
-cp $OUT/trace/t_kernel_stats.csv $PD/kernel_stats.csv; cp $OUT/bench_under_rocprof.json $PD/bench_under_rocprof.json
+
+
 echo done
