@@ -126,6 +126,11 @@ struct Stamps {
 #endif
 };
 
+// Diagnostic hook of the solve's stages (a probe build defines it; nothing otherwise)
+#ifndef GICP_SOLVE_STAMP
+#define GICP_SOLVE_STAMP(k) ((void)0)
+#endif
+
 // exact-rounding fp64 square distance, summed in axis order without FMA contraction
 // (the order a KD-tree accumulates it in)
 template <int D>
@@ -1124,6 +1129,13 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
     return 1.0;
 }
 
+// LDS the one-wave solve exchanges through
+template <int D>
+struct SolveLds {
+    static constexpr int NR = D * D, M = D == 2 ? 1 : 3;
+    double kc[D][NR], u[NR], hd[M][NR], f[NR];
+};
+
 template <int D>
 __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
@@ -2036,10 +2048,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 // (the M x M Newton system, the rotation update) runs redundantly in every lane, which keeps
 // the control flow uniform. Same iterates as the serial solver up to summation order.
 template <int D, class Sync>
-__device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync sync) {
+__device__ __forceinline__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, SolveLds<D>& sl, Sync sync) {
     using namespace solver_detail;
     constexpr int NS = D * (D + 1) / 2, NR = D * D, N1 = D + 1, M = D == 2 ? 1 : 3;
-    __shared__ double s_kc[D][NR], s_u[NR], s_hd[M][NR], s_f[NR];
+    auto& s_kc = sl.kc;
+    auto& s_u = sl.u;
+    auto& s_hd = sl.hd;
+    auto& s_f = sl.f;
     const int lane = threadIdx.x;
     const int i = lane < NR ? lane : 0;   // lanes >= NR shadow row 0 and never store
     SolveOut<D> out;
@@ -2062,12 +2077,12 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
         for (int b = 0; b < D; ++b) Rk[a * D + b] = Tk[a * N1 + b];
         tk[a] = Tk[a * N1 + D];
     }
-    double L[D][D];
+    double Ht[D][D], Hti[D][D];
 #pragma unroll
     for (int a = 0; a < D; ++a)
 #pragma unroll
-        for (int b = 0; b < D; ++b) L[a][b] = C[sym<D>(a, b)];
-    if (!chol<D>(L)) {
+        for (int b = 0; b < D; ++b) Ht[a][b] = C[sym<D>(a, b)];
+    if (!spd_inv<D>(Ht, Hti)) {
         out.ok = 0;
         return out;
     }
@@ -2076,12 +2091,12 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
         double rhs[D], x[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) rhs[a] = gt[a];
-        chol_solve<D>(L, rhs, kt);
+        sym_mul<D>(Hti, rhs, kt);
         // column i of K = Htt^-1 Htr on lane i
         const int ci = i / D, cj = i % D;
 #pragma unroll
         for (int b = 0; b < D; ++b) rhs[b] = B[sym<D>(ci, b) * D + cj];
-        chol_solve<D>(L, rhs, x);
+        sym_mul<D>(Hti, rhs, x);
         if (lane < NR)
 #pragma unroll
             for (int a = 0; a < D; ++a) s_kc[a][lane] = x[a];
@@ -2132,23 +2147,19 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
 #pragma unroll
     for (int k = 0; k < NR; ++k) R[k] = Rk[k];
     double ui;
+    GICP_SOLVE_STAMP(2);
     double f = eval(R, ui);
+    GICP_SOLVE_STAMP(3);
     double lam = 0.0;
     for (int it = 0; it < 100; ++it) {
-        double Dk[M][NR];
-#pragma unroll
-        for (int k = 0; k < M; ++k) gen_mul<D>(k, R, Dk[k]);
+        GICP_SOLVE_STAMP(4 + min(it, 3));
         if (lane < NR) {
             s_u[lane] = ui;
 #pragma unroll
-            for (int l = 0; l < M; ++l) {
-                double s = 0.0;
-#pragma unroll
-                for (int j = 0; j < NR; ++j) s += Hrow[j] * Dk[l][j];
-                s_hd[l][lane] = s;
-            }
+            for (int l = 0; l < M; ++l) s_hd[l][lane] = gdot<D>(l, R, Hrow);   // (H' vec(G_l R))_i
         }
         sync();
+        GICP_SOLVE_STAMP(8);
         // grad_k = 2 u.vec(G_k R) and the second-order term u.vec(1/2 (G_k G_l + G_l G_k) R) of the
         // serial solver, through P = R U^T (U = u as a D x D matrix): u.vec(X R) = tr(X P),
         // G_k G_l = e_l e_k^T - delta_kl I in 3-D and G^2 = -I in 2-D.
@@ -2177,13 +2188,13 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
         for (int k = 0; k < M; ++k)
 #pragma unroll
             for (int l = k; l < M; ++l) {
-                double s = 0.0;
-#pragma unroll
-                for (int j = 0; j < NR; ++j) s += Dk[k][j] * s_hd[l][j];
+                const double s = gdot<D>(k, R, s_hd[l]);
                 const double t2 = D == 2 ? -trP : 0.5 * (P[k][l] + P[l][k]) - (k == l ? trP : 0.0);
                 Hs[k][l] = Hs[l][k] = 2.0 * s + 2.0 * t2;
             }
-        sync();   // s_u / s_hd are rewritten next iteration
+        GICP_SOLVE_STAMP(9);
+        // (no barrier here: s_u / s_hd are rewritten only after the eval below, whose barriers order
+        // these reads; every path to the next iteration runs it)
         double gmax = 0.0, hscale = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -2191,10 +2202,10 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
             hscale = fmax(hscale, fabs(Hs[k][k]));
         }
         if (gmax == 0.0) break;
-        bool stepped = false, flat = false;
+        bool stepped = false, flat = false, quad = false;
         double wmax = 0.0;
         for (int tries = 0; tries < 60; ++tries) {
-            double Hd[M][M], ng[M], w[M];
+            double Hd[M][M], Hdi[M][M], ng[M], w[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) {
 #pragma unroll
@@ -2202,16 +2213,18 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
                 ng[k] = -grad[k];
             }
             double dd = 0.0;
-            bool ok = chol<M>(Hd);
+            bool ok = spd_inv<M>(Hd, Hdi);
             if (ok) {
-                chol_solve<M>(Hd, ng, w);
+                sym_mul<M>(Hdi, ng, w);
 #pragma unroll
                 for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
                 ok = dd < 0.0;
             }
+            GICP_SOLVE_STAMP(10);
             if (ok) {
                 double Rn[NR], un;
                 rot_update<D>(w, R, Rn);
+                GICP_SOLVE_STAMP(11);
                 const double fn = eval(Rn, un);
                 wmax = 0.0;
 #pragma unroll
@@ -2230,6 +2243,7 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
                         ui = un;
                     }
                     stepped = true;
+                    quad = fn <= f && lam == 0.0 && wmax < kQuadStop;   // (f = fn when accepted)
                     lam = lam > 0.0 ? lam * 0.1 : 0.0;
                     if (lam < 1e-12) lam = 0.0;
                     break;
@@ -2237,8 +2251,9 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
             }
             lam = lam == 0.0 ? 1e-9 : lam * 10.0;
         }
-        if (!stepped || flat || wmax < 1e-15) break;
+        if (!stepped || flat || quad || wmax < 1e-15) break;
     }
+    GICP_SOLVE_STAMP(12);
 #pragma unroll
     for (int a = 0; a < D; ++a) {
         double s = kt[a];
@@ -2255,28 +2270,30 @@ __device__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, Sync 
     return out;
 }
 
-// The inner solve (gicp.py:148-154) from a pass's statistics `st`, then the convergence test and pose
+// The inner solve (gicp.py:148-154) from a pass's statistics, then the convergence test and pose
 // update of gicp.py:155-167, on the device so iterations need no host sync.  Run by one wave (lanes
-// 0-63); `sync` orders that wave's LDS traffic.
+// 0-63); `sync` orders that wave's LDS traffic.  `Ls` is an LDS copy of the device state S (header
+// and statistics, loaded in one round trip): everything is read from it, only the results go to S.
 template <int D, class Sync>
-__device__ void solve_update(IterState* S, const double* st, Sync sync) {
+__device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl, Sync sync) {
     const int lane = threadIdx.x & 63;
     constexpr int NSX = nstat_ext(D);
+    const double* st = Ls->stats;
     if (lane < NSX) S->stats_solved[lane] = st[lane];
     if (lane + 64 < NSX) S->stats_solved[lane + 64] = st[lane + 64];
-    const SolveOut<D> r = solve_pose_wave<D>(st, S->T, sync);
-    sync();   // every lane has read S->T
+    const SolveOut<D> r = solve_pose_wave<D>(st, Ls->T, sl, sync);
     if (lane != 0) return;
-    const int it = S->iter;
+    const IterState* SR = Ls;   // the state as this launch found it
+    const int it = SR->iter;
     S->iter = it + 1;
     if (!r.ok) S->solve_fail = 1;
     S->loss = r.loss;
     constexpr int NSS = nstat(D);
-    S->pairs_total += st[NSS + 1];
+    S->pairs_total = SR->pairs_total + st[NSS + 1];
     const double cnt = st[NSS - 1];
-    const double mse = cnt > 0.0 ? st[NSS + 3] / cnt : 0.0;
+    const double mse = cnt > 0.0 ? st[NSS + 3] * solver_detail::recip(cnt) : 0.0;
     S->mse = mse;
-    if (!S->fixed && fabs(S->last_loss - r.loss) < S->tol) {   // gicp.py:160: stop before the update
+    if (!SR->fixed && fabs(SR->last_loss - r.loss) < SR->tol) {   // gicp.py:160: stop before the update
         S->converged = 1;
         S->converged_at = it;
         S->stop_reason = GICP_STOP_LOSS;
@@ -2286,7 +2303,7 @@ __device__ void solve_update(IterState* S, const double* st, Sync sync) {
     // PCL-style criteria on the increment dT = T_new T_old^-1 and the pass's MSE; PCL applies the
     // update and then tests, so these stop AFTER the update (include/gicp_hip.h GICP_STOP_*)
     int reason = GICP_STOP_NONE;
-    if (!S->fixed) {
+    if (!SR->fixed) {
         constexpr int N1 = D + 1;
         double tr = 0.0, tsq = 0.0;
 #pragma unroll
@@ -2296,17 +2313,17 @@ __device__ void solve_update(IterState* S, const double* st, Sync sync) {
             for (int b = 0; b < D; ++b) {
                 double dr = 0.0;   // (R_new R_old^T)[a][b]
 #pragma unroll
-                for (int c = 0; c < D; ++c) dr += r.T[a * N1 + c] * S->T[b * N1 + c];
+                for (int c = 0; c < D; ++c) dr += r.T[a * N1 + c] * SR->T[b * N1 + c];
                 if (a == b) tr += dr;
-                dta -= dr * S->T[b * N1 + D];
+                dta -= dr * SR->T[b * N1 + D];
             }
             tsq += dta * dta;
         }
         const double cosang = D == 3 ? 0.5 * (tr - 1.0) : 0.5 * tr;
-        const double dm = fabs(mse - S->prev_mse);
-        if (S->trans_eps > 0.0 && cosang >= S->rot_cos && tsq <= S->trans_eps) reason = GICP_STOP_TRANSFORM;
-        else if (S->fit_eps > 0.0 && dm < S->fit_eps) reason = GICP_STOP_ABS_MSE;
-        else if (S->rel_eps > 0.0 && dm / S->prev_mse < S->rel_eps) reason = GICP_STOP_REL_MSE;
+        const double dm = fabs(mse - SR->prev_mse);
+        if (SR->trans_eps > 0.0 && cosang >= SR->rot_cos && tsq <= SR->trans_eps) reason = GICP_STOP_TRANSFORM;
+        else if (SR->fit_eps > 0.0 && dm < SR->fit_eps) reason = GICP_STOP_ABS_MSE;
+        else if (SR->rel_eps > 0.0 && dm / SR->prev_mse < SR->rel_eps) reason = GICP_STOP_REL_MSE;
         S->prev_mse = mse;
     }
 #pragma unroll
@@ -2319,10 +2336,29 @@ __device__ void solve_update(IterState* S, const double* st, Sync sync) {
 }
 
 // One wave: solve_update on the statistics in the device state (after the multi-GPU all-reduce).
+// The state (header + statistics, ~110 doubles) comes into LDS with one load per lane in a single
+// round trip -- the statistics were just written by k_corr's last workgroup, likely on another XCD, so
+// each dependent global read costs a full memory latency; every later read is an LDS read.
 template <int D>
 __global__ void __launch_bounds__(64) k_solve(IterState* S) {
-    if (S->converged) return;
-    solve_update<D>(S, S->stats, [] { __syncthreads(); });
+    constexpr int NLOAD = (int)(offsetof(IterState, stats) / sizeof(double)) + nstat_ext(D);
+    static_assert(NLOAD <= 128, "state header + statistics: two loads per lane");
+    __shared__ IterState s_state;
+    __shared__ SolveLds<D> s_sl;
+    GICP_SOLVE_STAMP(0);
+    const int l = threadIdx.x;
+    const double* g = reinterpret_cast<const double*>(S);
+    double* sd = reinterpret_cast<double*>(&s_state);
+    const double v0 = g[l];
+    double v1 = 0.0;
+    if (l + 64 < NLOAD) v1 = g[l + 64];
+    sd[l] = v0;
+    if (l + 64 < NLOAD) sd[l + 64] = v1;
+    __syncthreads();
+    GICP_SOLVE_STAMP(1);
+    if (s_state.converged) return;
+    solve_update<D>(S, &s_state, s_sl, [] { __syncthreads(); });
+    GICP_SOLVE_STAMP(13);
 }
 
 // ---------------------------------------------------------------------------

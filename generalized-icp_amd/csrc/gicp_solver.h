@@ -26,6 +26,13 @@ namespace gicp {
 #define GICP_FLAT_EPS 8.0
 #endif
 constexpr double kFlatEps = GICP_FLAT_EPS * 2.220446049250313e-16;
+// After an accepted undamped Newton step of size |w| < kQuadStop the next step would be ~|w|^2
+// (quadratic convergence; the rotation's third derivative is O(1) relative to the Hessian), below
+// fp64 resolution of a rotation: stop instead of spending one more iteration to measure it
+#ifndef GICP_QUAD_STOP
+#define GICP_QUAD_STOP 1e-8
+#endif
+constexpr double kQuadStop = GICP_QUAD_STOP;
 
 template <int D>
 struct SolveOut {
@@ -41,43 +48,66 @@ GICP_HD constexpr int sym(int a, int b) {
     return a <= b ? a * D - a * (a - 1) / 2 + (b - a) : b * D - b * (b - 1) / 2 + (a - b);
 }
 
-// Cholesky solve of an N x N SPD system (lower factor in place); returns false if not SPD.
+// 1/x.  On the device v_rcp_f64 refined by two Newton-Raphson steps (within an ulp or two of the
+// quotient; a correctly rounded fp64 division is a ~10-instruction dependent chain with its own
+// scaling and fix-up, ~0.4 us of a one-wave solve); on the host the division itself.
+GICP_HD double recip(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+#else
+    return 1.0 / x;
+#endif
+}
+
+// Inverse of a symmetric N x N matrix (N <= 3, only the upper triangle is read) by its adjugate,
+// with the positive-definiteness test of the leading principal minors (Sylvester); false if not
+// SPD.  One reciprocal in all (a Cholesky factor costs N square roots and N(N+1)/2 + N^2 divisions,
+// which dominated the device solve: one wave, fp64 div/sqrt are ~10-instruction dependent chains).
+// The matrices here (the translation block of the Hessian, the damped 3 x 3 Newton system) are
+// small and well conditioned.
 template <int N>
-GICP_HD bool chol(double (&M)[N][N]) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        double s = M[j][j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) s -= M[j][k] * M[j][k];
-        if (!(s > 0.0)) return false;
-        const double r = sqrt(s);
-        M[j][j] = r;
-#pragma unroll
-        for (int i = j + 1; i < N; ++i) {
-            double t = M[i][j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) t -= M[i][k] * M[j][k];
-            M[i][j] = t / r;
-        }
+GICP_HD bool spd_inv(const double (&M)[N][N], double (&Mi)[N][N]) {
+    static_assert(N >= 1 && N <= 3, "spd_inv: N <= 3");
+    if constexpr (N == 1) {
+        if (!(M[0][0] > 0.0)) return false;
+        Mi[0][0] = recip(M[0][0]);
+    } else if constexpr (N == 2) {
+        const double det = M[0][0] * M[1][1] - M[0][1] * M[0][1];
+        if (!(M[0][0] > 0.0 && det > 0.0)) return false;
+        const double id = recip(det);
+        Mi[0][0] = M[1][1] * id;
+        Mi[1][1] = M[0][0] * id;
+        Mi[0][1] = Mi[1][0] = -M[0][1] * id;
+    } else {
+        const double c00 = M[1][1] * M[2][2] - M[1][2] * M[1][2];
+        const double c01 = M[0][2] * M[1][2] - M[0][1] * M[2][2];
+        const double c02 = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+        const double c11 = M[0][0] * M[2][2] - M[0][2] * M[0][2];
+        const double c12 = M[0][2] * M[0][1] - M[0][0] * M[1][2];
+        const double c22 = M[0][0] * M[1][1] - M[0][1] * M[0][1];
+        const double det = M[0][0] * c00 + M[0][1] * c01 + M[0][2] * c02;
+        if (!(M[0][0] > 0.0 && c22 > 0.0 && det > 0.0)) return false;
+        const double id = recip(det);
+        Mi[0][0] = c00 * id;
+        Mi[0][1] = Mi[1][0] = c01 * id;
+        Mi[0][2] = Mi[2][0] = c02 * id;
+        Mi[1][1] = c11 * id;
+        Mi[1][2] = Mi[2][1] = c12 * id;
+        Mi[2][2] = c22 * id;
     }
     return true;
 }
 template <int N>
-GICP_HD void chol_solve(const double (&L)[N][N], const double (&b)[N], double (&x)[N]) {
-    double y[N];
+GICP_HD void sym_mul(const double (&Mi)[N][N], const double (&b)[N], double (&x)[N]) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        double s = b[i];
+        double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
-        y[i] = s / L[i][i];
-    }
-#pragma unroll
-    for (int i = N - 1; i >= 0; --i) {
-        double s = y[i];
-#pragma unroll
-        for (int k = i + 1; k < N; ++k) s -= L[k][i] * x[k];
-        x[i] = s / L[i][i];
+        for (int k = 0; k < N; ++k) s += Mi[i][k] * b[k];
+        x[i] = s;
     }
 }
 
@@ -93,26 +123,23 @@ GICP_HD void rot_update(const double* w, const double (&R)[D * D], double (&Rn)[
         }
     } else {
         const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-        const double th = sqrt(th2);
         double s1, s2;
-        if (th < 0.25) {
-            // sin(th)/th and (1-cos th)/th^2 by their series: truncation < th^12/6e9 < 1e-17 here,
-            // and no libm sin/cos on the device's single-wave solve (the Newton steps are small)
+        if (th2 < 0.0625) {
+            // sin(th)/th and (1-cos th)/th^2 by their series in th^2 (th < 0.25): truncation
+            // < th^12/6e9 < 1e-17 here, and neither libm sin/cos nor a square root on the device's
+            // single-wave solve (the Newton steps are small)
             s1 = 1.0 + th2 * (-1.0 / 6 + th2 * (1.0 / 120 + th2 * (-1.0 / 5040 + th2 * (1.0 / 362880 + th2 * (-1.0 / 39916800)))));
             s2 = 0.5 + th2 * (-1.0 / 24 + th2 * (1.0 / 720 + th2 * (-1.0 / 40320 + th2 * (1.0 / 3628800 + th2 * (-1.0 / 479001600)))));
         } else {
+            const double th = sqrt(th2);
             s1 = sin(th) / th;
             s2 = (1.0 - cos(th)) / th2;
         }
-        const double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-        double E[9];
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                const double k2 = K[a * 3] * K[b] + K[a * 3 + 1] * K[3 + b] + K[a * 3 + 2] * K[6 + b];
-                E[a * 3 + b] = (a == b ? 1.0 : 0.0) + s1 * K[a * 3 + b] + s2 * k2;
-            }
+        // exp([w]) = cos(th) I + s1 [w]x + s2 w w^T  ([w]x^2 = w w^T - th^2 I, cos th = 1 - s2 th^2)
+        const double c = 1.0 - s2 * th2;
+        const double E[9] = {c + s2 * w[0] * w[0], s2 * w[0] * w[1] - s1 * w[2], s2 * w[0] * w[2] + s1 * w[1],
+                             s2 * w[1] * w[0] + s1 * w[2], c + s2 * w[1] * w[1], s2 * w[1] * w[2] - s1 * w[0],
+                             s2 * w[2] * w[0] - s1 * w[1], s2 * w[2] * w[1] + s1 * w[0], c + s2 * w[2] * w[2]};
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
@@ -150,6 +177,24 @@ GICP_HD void gen_mul(int k, const double (&R)[D * D], double (&out)[D * D]) {
     }
 }
 
+// sum_j vec(G_k R)_j v_j with only the six nonzero entries of G_k R (3-D; the zeros would still cost
+// an FMA each: 0 * x is not foldable without fast-math)
+template <int D>
+GICP_HD double gdot(int k, const double (&R)[D * D], const double* v) {
+    double s = 0.0;
+    if constexpr (D == 2) {
+        s = -R[2] * v[0] - R[3] * v[1] + R[0] * v[2] + R[1] * v[3];
+    } else {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            if (k == 0) s += R[3 + b] * v[6 + b] - R[6 + b] * v[3 + b];
+            else if (k == 1) s += R[6 + b] * v[b] - R[b] * v[6 + b];
+            else s += R[b] * v[3 + b] - R[3 + b] * v[b];
+        }
+    }
+    return s;
+}
+
 }  // namespace solver_detail
 
 // Minimise the quadratic of `st` (layout DESIGN.md §4) over SE(D) from Tk.
@@ -178,13 +223,13 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
         for (int b = 0; b < D; ++b) Rk[a * D + b] = Tk[a * N1 + b];
         tk[a] = Tk[a * N1 + D];
     }
-    // Htt (Cholesky), K = Htt^-1 Htr, kt = Htt^-1 gt
-    double L[D][D];
+    // Htt^-1, K = Htt^-1 Htr, kt = Htt^-1 gt
+    double Ht[D][D], Hti[D][D];
 #pragma unroll
     for (int a = 0; a < D; ++a)
 #pragma unroll
-        for (int b = 0; b < D; ++b) L[a][b] = C[sym<D>(a, b)];
-    if (!chol<D>(L)) {
+        for (int b = 0; b < D; ++b) Ht[a][b] = C[sym<D>(a, b)];
+    if (!spd_inv<D>(Ht, Hti)) {
         out.ok = 0;
         return out;
     }
@@ -193,7 +238,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
         double rhs[D], x[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) rhs[a] = gt[a];
-        chol_solve<D>(L, rhs, x);
+        sym_mul<D>(Hti, rhs, x);
 #pragma unroll
         for (int a = 0; a < D; ++a) kt[a] = x[a];
 #pragma unroll
@@ -201,7 +246,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
             const int ci = c / D, cj = c % D;   // column (ci, cj) of Htr: H[t_b][(ci,cj)] = B[sym(ci,b)][cj]
 #pragma unroll
             for (int b = 0; b < D; ++b) rhs[b] = B[sym<D>(ci, b) * D + cj];
-            chol_solve<D>(L, rhs, x);
+            sym_mul<D>(Hti, rhs, x);
 #pragma unroll
             for (int a = 0; a < D; ++a) Kc[a][c] = x[a];
         }
@@ -298,11 +343,11 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
             hscale = fmax(hscale, fabs(Hs[k][k]));
         }
         if (gmax == 0.0) break;
-        bool stepped = false, flat = false;
+        bool stepped = false, flat = false, quad = false;
         double wmax = 0.0;
         for (int tries = 0; tries < 60; ++tries) {
             GICP_SOLVER_PROBE_TRY();
-            double Hd[M][M], ng[M], w[M];
+            double Hd[M][M], Hdi[M][M], ng[M], w[M];
 #pragma unroll
             for (int k = 0; k < M; ++k) {
 #pragma unroll
@@ -310,9 +355,9 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
                 ng[k] = -grad[k];
             }
             double dd = 0.0;
-            bool ok = chol<M>(Hd);
+            bool ok = spd_inv<M>(Hd, Hdi);
             if (ok) {
-                chol_solve<M>(Hd, ng, w);
+                sym_mul<M>(Hdi, ng, w);
 #pragma unroll
                 for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
                 ok = dd < 0.0;
@@ -337,6 +382,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
                         f = fn;
                     }
                     stepped = true;
+                    quad = fn <= f && lam == 0.0 && wmax < kQuadStop;   // (f = fn when accepted)
                     lam = lam > 0.0 ? lam * 0.1 : 0.0;
                     if (lam < 1e-12) lam = 0.0;
                     break;
@@ -344,7 +390,7 @@ GICP_HD SolveOut<D> solve_pose_t(const double* st, const double* Tk) {
             }
             lam = lam == 0.0 ? 1e-9 : lam * 10.0;
         }
-        if (!stepped || flat || wmax < 1e-15) break;
+        if (!stepped || flat || quad || wmax < 1e-15) break;
     }
     // t from the eliminated block
 #pragma unroll
