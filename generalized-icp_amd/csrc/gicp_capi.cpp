@@ -739,6 +739,16 @@ void ensure_workspace(gicp_ctx* c) {
     }
 }
 
+// The largest double x with sqrt(x) <= dc (sqrt correctly rounded, as on the device), so the accept
+// test of gicp.py:136, !(distance > d_c) with distance = sqrt(d2), is exactly d2 <= accept_d2_max(d_c)
+double accept_d2_max(double dc) {
+    if (!(dc >= 0.0) || std::isinf(dc)) return dc;   // d_c = +inf accepts everything; NaN nothing
+    double x = dc * dc;
+    while (std::sqrt(x) > dc) x = std::nextafter(x, 0.0);
+    while (std::sqrt(std::nextafter(x, INFINITY)) <= dc) x = std::nextafter(x, INFINITY);
+    return x;
+}
+
 // kernel arguments of a pass (the pose comes from the device state)
 CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     const int d = c->src.dim;
@@ -755,6 +765,7 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.single_pass = single_pass;
     const double dc = c->psrc.max_distance_correspondence;
     a.dc = dc;
+    a.dc2_max = accept_d2_max(dc);
     // with certificates the screen reaches kappa past d_c, so an empty lane's radius outlasts small moves
     const double kappa = c->use_certs ? c->kappa_frac * dc : 0.0;
     a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc + kappa);

@@ -162,6 +162,7 @@ struct CorrArgs {
     float search2;            // fp32 screen bound (d_c^2 + margins)
     float gap_slack;          // rounding slack S of the box tests (search radius + 2 rho_t, x 2^-19)
     double dc;                // d_c, fp64, inclusive (distance > d_c rejects)
+    double dc2_max;           // the largest double x with sqrt(x) <= d_c: "sqrt(d2) > d_c" <=> d2 > dc2_max
     Margin mg;
     int32_t* hint;            // [src.ntiles] best target tile of the previous pass
     double* partials;         // [gridDim.x][nstat_ext] workgroup partials

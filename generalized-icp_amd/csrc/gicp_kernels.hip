@@ -460,10 +460,13 @@ struct WaveStage {
     double x64[kTile], y64[kTile], z64[kTile];    // fp64 coordinates (covariance sums, fallback)
     int32_t perm[kTile];                          // original indices (fallback tie-break)
 };
-// statistics transpose image: 16 points x 16 u-terms and 16 x 16 v-terms (XOR-swizzled 16-B chunks)
+// statistics transpose image of 16 points: u[term][point] and v[term][point], rows padded to 17 doubles
+// (a term's 16 points are written by 16 lanes to consecutive words; the MFMA operand reads of a row
+// group spread over the banks)
+constexpr int kStatRow = 17;
 struct WaveStat {
-    double u[16 * 16];
-    double v[16 * 16];
+    double u[16 * kStatRow];
+    double v[16 * kStatRow];
 };
 union __attribute__((aligned(16))) WaveLds {
     WaveStage t;
@@ -532,6 +535,84 @@ __device__ __forceinline__ void stage_f32_from(const float4& v, WaveLds& L) {
     L.t.z[l] = v.z;
     wave_sync();
 }
+// k_corr's full walk: traverse_c's order and culling, but each lane of a candidate block holds its
+// tile's box gap and (start, count), so a candidate's coordinates are requested together with its
+// metadata (visit_pre(T, &coords): one memory round trip per visited tile instead of two), and
+// candidates the shrinking bound has put out of reach are dropped before they are visited (the test the
+// block entry applied, repeated with the current bound; a tile it drops could not have been within
+// any lane's bound).
+template <int D, class VisitPre, class WB, class Collect, class Cnt = NoCount>
+__device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, int seed, VisitPre&& visit_pre,
+                                       WB&& wave_bound, float skin, Collect&& collect, Cnt* cnt = nullptr) {
+    const int l = lane_id();
+    auto infl = [&](float w) -> float {
+        if (skin <= 0.f || w < 0.f) return w;
+        const float r = __builtin_amdgcn_sqrtf(w) * 1.0001f + skin;
+        return r * r;
+    };
+    float wb = wave_bound();
+    float wbi = infl(wb);
+    if (seed >= 0) {
+        collect(seed);
+        if (visit_pre(seed, nullptr)) {
+            wb = wave_bound();
+            wbi = infl(wb);
+        }
+    }
+    typedef __attribute__((address_space(4))) const BlockInfo* ConstBlocks;
+    const ConstBlocks cb0 = (ConstBlocks)(uintptr_t)db.blocks + db.nblocks;
+    for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
+        {
+            const ConstBlocks sb = cb0 + (b0 / kWave);
+            const double c[3] = {sb->c[0], sb->c[1], sb->c[2]};
+            const float h[3] = {sb->h[0], sb->h[1], sb->h[2]};
+            if (!__builtin_amdgcn_readfirstlane((int)(gap2_box<D>(q, c, h) <= wbi))) continue;   // uniform
+        }
+        if (cnt) cnt->count(5);
+        const int b = b0 + l;
+        bool cb = false;
+        if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wbi;
+        uint64_t bm = __ballot(cb);
+        while (bm) {
+            const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
+            bm &= bm - 1;
+            const int first = db.blocks[bb].first, nt = db.blocks[bb].ntiles;
+            if (cnt) cnt->count(6);
+            const int t = first + l;
+            bool ct = false;
+            float g2 = 3e38f;
+            uint32_t sc6 = 0;   // (start << 6) | (count - 1): one register (gicp_set_* keep n < 2^26)
+            if (l < nt && t != seed) {
+                g2 = gap2_box<D>(q, db.tiles[t].c, db.tiles[t].h);
+                ct = g2 <= wbi;
+                sc6 = ((uint32_t)db.tiles[t].start << 6) | (uint32_t)(db.tiles[t].count - 1);
+            }
+            if (skin > 0.f) {
+                uint64_t cm = __ballot(ct);
+                while (cm) {
+                    collect(first + __ffsll((unsigned long long)cm) - 1);
+                    cm &= cm - 1;
+                }
+            }
+            uint64_t tm = __ballot(g2 <= wb);
+            auto pick = [&]() -> int { return tm ? __ffsll((unsigned long long)tm) - 1 : -1; };
+            auto coords = [&](int kk) {
+                const uint32_t v = __builtin_amdgcn_readlane(sc6, kk);
+                return load_rel(db, (int)(v >> 6), (int)(v & 63u) + 1);
+            };
+            for (int k = pick(); k >= 0; k = pick()) {
+                tm &= ~(1ull << k);
+                const float4 pv = coords(k);   // in flight with the tile's metadata load in visit_pre
+                if (visit_pre(first + k, &pv)) {
+                    wb = wave_bound();
+                    wbi = infl(wb);
+                    tm &= __ballot(g2 <= wb);
+                }
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void stage_f64(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
     const int l = lane_id();
     double4 v;
@@ -1254,7 +1335,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 }
                 dc2 += m * m;
             }
-            return (float)(sqrt(dc2) + sqrt(dr2) * (double)st.radius) * 1.0001f + 1e-30f;
+            // an upper bound: fp32 square roots of the rounded sums, covered by the 1.0001 factor
+            return (__builtin_amdgcn_sqrtf((float)dc2) + __builtin_amdgcn_sqrtf((float)dr2) * st.radius) * 1.0001f + 1e-30f;
         };
 
         // ---- per-point nearest-neighbour certificates ------------------------
@@ -1586,8 +1668,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 if (l == ncol) cent = Tt;
                 ++ncol;
             };
-            traverse_c<D>(tg, q, seed, visit, [&]() { return wave_maxf(lb); }, lists ? skin : 0.f,
-                          collect, &S);
+            walk_c<D>(tg, q, seed, visit_pre, [&]() { return wave_maxf(lb); }, lists ? skin : 0.f,
+                      collect, &S);
             if (lists) {
                 const float wbf = wave_maxf(lb);
                 const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + skin : 0.f;
@@ -1747,9 +1829,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (skip_walk) source_point(s4e);
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
-            const double dist = sqrt(d2e);
-            if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = dist;
-            if (!(dist > A.dc)) {  // gicp.py:136: reject only if distance > d_c
+            if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = sqrt(d2e);
+            // gicp.py:136: reject only if distance > d_c; sqrt(d2) > d_c <=> d2 > dc2_max (host-computed,
+            // sqrt is correctly rounded and monotone), so no square root here
+            if (d2e <= A.dc2_max) {
                 on = true;
                 const double mt[3] = {ct.y, ct.z, ct.w};
                 if (A.cov_model == GICP_COV_POINT_TO_POINT) {          // C_s = 0, C_t = I: W = I
@@ -1779,9 +1862,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         S[a][b] = (a == b ? cs.x + ct.x : 0.0) - mr[a] * mr[b] - mt[a] * mt[b];
                 if constexpr (D == 2) {
                     const double det = S[0][0] * S[1][1] - S[0][1] * S[1][0];
-                    W[0][0] = S[1][1] / det;
-                    W[1][1] = S[0][0] / det;
-                    W[0][1] = W[1][0] = -S[0][1] / det;
+                    const double id = solver_detail::recip(det);
+                    W[0][0] = S[1][1] * id;
+                    W[1][1] = S[0][0] * id;
+                    W[0][1] = W[1][0] = -S[0][1] * id;
                 } else {
                     const double c00 = S[1][1] * S[2][2] - S[1][2] * S[2][1];
                     const double c01 = S[0][2] * S[2][1] - S[0][1] * S[2][2];
@@ -1790,7 +1874,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     const double c12 = S[0][2] * S[1][0] - S[0][0] * S[1][2];
                     const double c22 = S[0][0] * S[1][1] - S[0][1] * S[1][0];
                     const double det = S[0][0] * c00 + S[0][1] * c01 + S[0][2] * c02;
-                    const double id = 1.0 / det;
+                    const double id = solver_detail::recip(det);   // (refined v_rcp_f64, within ~1 ulp)
                     W[0][0] = c00 * id;
                     W[0][1] = W[1][0] = c01 * id;
                     W[0][2] = W[2][0] = c02 * id;
@@ -1841,64 +1925,61 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         amb = amb && q.valid;
     }
 
-    {   // sum |r|^2 of the accepted points (PCL's MSE numerator, extended slot): a plain wave sum here
-        // keeps r2 dead before the statistics GEMM (as a GEMM row it would cost 4 VGPRs and a wave/SIMD)
-        double t = on ? r2 : 0.0;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if (l == 0) s_wstat[w][NSS + 3] += t;
-    }
     S.mark(5);
     // ---- wave reduction of the statistics: a 16x16x64 fp64 GEMM on MFMA ---------------------
-    // stats[p][q] = sum over lanes of u_p v_q with u = (W sym, W r, r^T W r, 1), v = (s s sym, s, 1)
-    // (DESIGN.md §4).  Points are transposed through LDS 16 at a time (rows of 16 doubles, 16-B
-    // chunks XOR-swizzled by row so the 8-lane write groups and 32-lane read groups are conflict-free);
-    // lane l feeds A[p = l&15][k = l>>4] / B[k][q = l&15] of v_mfma_f64_16x16x4_f64.
+    // stats[p][q] = sum over lanes of u_p v_q with u = (W sym, W r, r^T W r, 1, |r|^2), v = (s s sym, s,
+    // 1).  Points are transposed through LDS 16 at a time as u[term][point] /
+    // v[term][point]: lane = point writes its terms to one column (every address a constant offset of
+    // one base, no per-write address arithmetic), lane l reads A[p = l&15][k = l>>4] /
+    // B[k][q = l&15] of v_mfma_f64_16x16x4_f64 from row l&15 at a constant offset per MFMA.
     {
         constexpr int NS = D * (D + 1) / 2;
+        constexpr int NU = NS + D + 3;   // u terms in use (the rest of the 16 rows stay zero)
+        constexpr int NV = NS + D + 1;   // v terms in use
         // u_k / v_k of this lane's point, formed at the write (k is a compile-time constant there)
+        // W, W r and r^T W r are exact zeros unless `on` (never written otherwise), so only the count
+        // entry of u needs the mask: a rejected or padding lane's u is 0 and its finite v adds nothing
         auto uel = [&](int k) -> double {
-            if (!on) return 0.0;
             if (k < NS) return W[StatIdx<D>::pa(k)][StatIdx<D>::pb(k)];
             if (k < NS + D) return wr[k - NS];
             if (k == NS + D) return rwr;
-            if (k == NS + D + 1) return 1.0;
-            return 0.0;
+            if (k == NS + D + 1) return on ? 1.0 : 0.0;
+            return r2;   // |r|^2 (0 unless on): PCL's MSE numerator, extended slot NSS + 3
         };
         auto vel = [&](int k) -> double {
-            if (!on) return 0.0;
             if (k < NS) return sv[StatIdx<D>::pa(k)] * sv[StatIdx<D>::pb(k)];
             if (k < NS + D) return sv[k - NS];
-            if (k == NS + D) return 1.0;
-            return 0.0;
+            return 1.0;
         };
         typedef double d4v __attribute__((ext_vector_type(4)));
         d4v acc = {0.0, 0.0, 0.0, 0.0};
         WaveStat& X = s_lds[w].st;
-        const int row = l & 15;
-        // points that contribute nothing (rejected, or the tile's padding lanes) have u = v = 0: a group
+        // points that contribute nothing (rejected, or the tile's padding lanes) have u = 0: a group
         // of 16 or an MFMA's 4 points with none accepted adds exact zeros and is skipped (uniform test)
         const uint64_t onm = __ballot(on);
         wave_sync();
+        if (onm) {   // the unused term rows read as zeros (this LDS held the walk's staging until now)
+            for (int k = l; k < (16 - NU) * kStatRow; k += 64) X.u[NU * kStatRow + k] = 0.0;
+            for (int k = l; k < (16 - NV) * kStatRow; k += 64) X.v[NV * kStatRow + k] = 0.0;
+        }
+        double* const wu = &X.u[l & 15];
+        double* const wv = &X.v[l & 15];
+        const double* const ru = &X.u[(l & 15) * kStatRow + (l >> 4)];
+        const double* const rv = &X.v[(l & 15) * kStatRow + (l >> 4)];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (((onm >> (16 * g)) & 0xFFFFull) == 0) continue;
             if ((l >> 4) == g) {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const int off = row * 16 + 2 * (c ^ (row & 7));
-                    *reinterpret_cast<double2*>(&X.u[off]) = make_double2(uel(2 * c), uel(2 * c + 1));
-                    *reinterpret_cast<double2*>(&X.v[off]) = make_double2(vel(2 * c), vel(2 * c + 1));
-                }
+                for (int k = 0; k < NU; ++k) wu[k * kStatRow] = uel(k);
+#pragma unroll
+                for (int k = 0; k < NV; ++k) wv[k * kStatRow] = vel(k);
             }
             wave_sync();
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 if (((onm >> (16 * g + 4 * cc)) & 0xFull) == 0) continue;
-                const int r = 4 * cc + (l >> 4);
-                const int e = l & 15;
-                const int off = r * 16 + 2 * ((e >> 1) ^ (r & 7)) + (e & 1);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X.u[off], X.v[off], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ru[4 * cc], rv[4 * cc], acc, 0, 0, 0);
             }
             wave_sync();
         }
@@ -1916,6 +1997,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 else if (qq == NS + D) idx = NS * NS + NS * D + NS + D * D + (p - NS);
             } else if (qq == NS + D && p <= NS + D + 1) {
                 idx = NS * NS + NS * D + NS + D * D + D + (p - NS - D);   // c0, count
+            } else if (qq == NS + D && p == NS + D + 2) {
+                idx = NSS + 3;                                            // sum |r|^2
             }
             if (idx >= 0) s_wstat[w][idx] += acc[j];   // each (p,q) has one owner lane: no race
         }
