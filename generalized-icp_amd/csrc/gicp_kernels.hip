@@ -1214,7 +1214,7 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 template <int D>
 struct SolveLds {
     static constexpr int NR = D * D, M = D == 2 ? 1 : 3;
-    double kc[D][NR], u[NR], hd[M][NR], f[NR];
+    double kc[D][NR], u[NR], hd[M][NR], f[2][NR];   // f double-buffered: one barrier per loss evaluation
 };
 
 template <int D>
@@ -2208,6 +2208,7 @@ __device__ __forceinline__ SolveOut<D> solve_pose_wave(const double* st, const d
     for (int a = 0; a < D; ++a) c0p -= gt[a] * kt[a];
 
     // loss at R (phi of the serial solver) and, on lane i, u_i = (H' dr - g')_i
+    int fbuf = 0;
     auto eval = [&](const double (&Rv)[NR], double& ui) {
         double hi = 0.0, dri = 0.0;
 #pragma unroll
@@ -2217,21 +2218,25 @@ __device__ __forceinline__ SolveOut<D> solve_pose_wave(const double* st, const d
             dri = j == i ? dr : dri;
         }
         ui = hi - gpi;
-        if (lane < NR) s_f[lane] = dri * hi - 2.0 * gpi * dri;
+        // alternate buffers: a buffer is rewritten two evaluations later, and every path between
+        // passes a barrier after its reads (this eval's or the next iteration's), so no second one here
+        double* const fb = s_f[fbuf];
+        fbuf ^= 1;
+        if (lane < NR) fb[lane] = dri * hi - 2.0 * gpi * dri;
         sync();
         double f = c0p;
 #pragma unroll
-        for (int j = 0; j < NR; ++j) f += s_f[j];
-        sync();
+        for (int j = 0; j < NR; ++j) f += fb[j];
         return f;
     };
 
     double R[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k) R[k] = Rk[k];
-    double ui;
+    // at R = R_k: dr = 0, so u_i = -g'_i and the loss is c0' exactly (what eval(R_k) would return)
+    double ui = -gpi;
     GICP_SOLVE_STAMP(2);
-    double f = eval(R, ui);
+    double f = c0p;
     GICP_SOLVE_STAMP(3);
     double lam = 0.0;
     for (int it = 0; it < 100; ++it) {
