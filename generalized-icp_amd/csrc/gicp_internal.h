@@ -73,7 +73,8 @@ struct DevCloud {
     // neighbour graph (target only; null when not built), DESIGN.md §3c.  Row i is one 128-B line:
     // dword 0 r(i) (fp32: every target t != i with |x_t - x_i| < r is in the row), dword 1 the scale s,
     // then kGraphK entries of 3 int16 (x_t - x_i) / s, rounded to nearest (|error| <= s / 2 per
-    // axis); an unused entry has x = -32768.  nbi[i][k] = sorted index of entry k (-1 unused).
+    // axis); an unused entry repeats the last real one (offset 0 in an empty row).  nbi[i][k] = sorted index of
+    // entry k (-1 unused).
     const uint4* nbq;         // [n][8]
     const int32_t* nbi;       // [n][kGraphK]
     int64_t n;

@@ -1142,8 +1142,12 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
     w[0] = __float_as_uint(h.x);
     w[1] = __float_as_uint(s);
     int16_t* e = reinterpret_cast<int16_t*>(w + 2);
+    // unused entries (k >= cnt) repeat the last real entry (or the node itself, offset 0, in an empty
+    // row), so the descent needs no per-entry validity test: a repeated entry never becomes the
+    // strictly nearer candidate and at most makes the runner-up equal the winner, which the descent
+    // treats as a near tie resolved exactly over the real entries (nbi = -1 marks the repeats)
+    int16_t q[3] = {0, 0, 0};
     for (int k = 0; k < kGraphK; ++k) {
-        int16_t q[3] = {-32768, 0, 0};
         int idx = -1;
         if (k < cnt) {
             const float4 v = nb[i * kGraphK + k];
@@ -1426,8 +1430,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         const float dx = fmaf(-sc, (float)c3[0], qr[0]);
                         const float dy = fmaf(-sc, (float)c3[1], qr[1]);
                         const float dz = fmaf(-sc, (float)c3[2], qr[2]);
-                        float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                        dd = c3[0] == -32768 ? 3e38f : dd;   // unused entry
+                        // (an unused entry repeats a real one, k_graph_pack: no validity test here)
+                        const float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
                         if (dd < b1) {
                             b2 = b1;
                             b1 = dd;
