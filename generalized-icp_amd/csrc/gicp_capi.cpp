@@ -311,6 +311,9 @@ struct gicp_ctx {
     size_t cap_cj = 0, cap_cg = 0, cap_cp = 0;
     bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
     bool use_graph = true;            // GICP_NO_GRAPH=1: no target neighbour graph, no graph descent
+    int unit_map = 0;                 // k_corr workgroup -> unit map (CorrArgs::unit_map, GICP_UNIT_MAP)
+    int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
+    int moving_iters = 5;             // (GICP_MOVING_ITERS)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
@@ -759,6 +762,7 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.q_end = c->q_end;
     a.sh_skip = (c->nshards - 1) * kShardChunk;
     a.sh_first = c->shard * kShardChunk;
+    a.unit_map = c->unit_map;
     a.state = c->d_state;
     a.tickets = c->d_tickets;
     a.gpart = c->d_gpart;
@@ -990,6 +994,9 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_NO_GRAPH")) c->use_graph = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_UNIT_MAP")) c->unit_map = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -1284,6 +1291,7 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
                                    c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 8);
             for (int b = 0; b < B; ++b) {
                 CorrArgs a = corr_args(c, 0);
+                if (enq + b < c->moving_iters) a.unit_map = c->moving_map;
                 const bool ev = timing && (enq + b) % kEvStride == kEvOffset;
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b], st));
                 if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));

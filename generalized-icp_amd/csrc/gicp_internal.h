@@ -156,6 +156,9 @@ struct CorrArgs {
     // source shards (interleaved by kShardChunk units): this rank's unit u is the cloud's unit
     // u + (u / kShardChunk) sh_skip + sh_first, sh_skip = (G - 1) kShardChunk, sh_first = r kShardChunk
     int32_t sh_skip, sh_first;
+    // workgroup -> unit map: 0 = XCD stripes (XCD x takes the contiguous eighth x), C > 0 = chunks of C
+    // units dealt round-robin to the XCDs (1 = identity)
+    int32_t unit_map;
     IterState* state;         // pose in, statistics out
     uint32_t* tickets;        // [kMaxGroups + 1] arrival counters, zero between launches (self-resetting)
     double* gpart;            // [kMaxGroups][nstat_ext] group partials

@@ -1275,7 +1275,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     // walking set changes from pass to pass)
     const int nunits = (int)gridDim.x, q8 = nunits / 8;
     int unit = (int)blockIdx.x;
-    if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
+    if (A.unit_map == 0) {
+        if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
+    } else {   // the k-th workgroup of XCD x takes unit k % C of the XCD's (k / C)-th chunk of C units
+        const int C = A.unit_map, full = nunits / (8 * C) * (8 * C);
+        if (unit < full) unit = (((unit >> 3) / C) * 8 + (unit & 7)) * C + (unit >> 3) % C;
+    }
     unit = __builtin_amdgcn_readfirstlane(unit);
     // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
     int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # bench.py (default workload, cold start) under environment variants, interleaved, one GPU call:
 #   scripts/bench_variants.sh OUTDIR REPS "ENV1" "ENV2" ...      (use "X=0" for the default build)
+#   BENCH_ARGS="--n 100000" selects another workload
 set -o pipefail
 OUT=gpurun_out/$1; REPS=$2; shift 2
 mkdir -p $OUT
@@ -8,7 +9,7 @@ for r in $(seq 1 $REPS); do
   i=0
   for v in "$@"; do
     i=$((i+1))
-    env $v timeout -k 10 200 python bench.py --no-cpu-baseline > $OUT/v${i}_r$r.json 2> $OUT/v${i}_r$r.err || { echo "variant $v failed"; tail $OUT/v${i}_r$r.err; exit 1; }
+    env $v timeout -k 10 200 python bench.py --no-cpu-baseline $BENCH_ARGS > $OUT/v${i}_r$r.json 2> $OUT/v${i}_r$r.err || { echo "variant $v failed"; tail $OUT/v${i}_r$r.err; exit 1; }
   done
 done
 python - "$OUT" "$REPS" "$@" <<'PY'

@@ -29,7 +29,7 @@ for rep in range(2):
         step = np.linalg.norm(Tn[:3, 3] - T[:3, 3])
         rows.append(f"pass {k:2d} {dt*1e6:7.0f} us  step {step*100:7.3f} cm  pairs/pt {inf['pairs']/n:7.1f}  "
                     f"rebuilds {int(inf['list_rebuilds']):6d}  graph {int(inf['graph_proved']):8d}  "
-                    f"walked {int(inf['walked_tiles']):6d}  amb {int(inf['ambiguous'])}")
+                    f"walked {int(inf['walked_tiles']):6d}  amb {int(inf['ambiguous'])}  acc {int(st[73])}")
         T = Tn
     if rep == 1:
         print("\n".join(rows))
