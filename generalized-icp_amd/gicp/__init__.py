@@ -515,8 +515,8 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     eye = np.eye(d + 1)
     moved_source = False   # faithful mode: the engine holds a transformed copy of the source
     for it in range(int(max_iterations)):
-        moved = apply_transformation(src, T)                       # gicp.py:119
         if mode == "faithful":
+            moved = apply_transformation(src, T)                   # gicp.py:119
             if it > 0 or T0 is not None:
                 eng.set_source(moved, p)                           # gicp.py:120, on the GPU
                 moved_source = True
@@ -563,7 +563,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
                 qt = np.zeros((int(ok.sum()), d))
                 m = top_t[ok] >= 0
                 qt[m] = tgt[top_t[ok][m]]
-                hw_s.append(moved[top_s[ok]])
+                hw_s.append(apply_transformation(src[top_s[ok]], T))   # gicp.py:119,171: the 5 rows only
                 hw_t.append(qt)
         offset = new_offset
         stop = None
