@@ -38,7 +38,7 @@ hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t);
 hipError_t launch_graph(const GraphArgs&, int, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
-hipError_t launch_top_weights(const double*, const int64_t*, int64_t, int, double*, int32_t*, int, double*, int64_t*,
+hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
 int corr_grid(int q_tiles, int shard, int nshards);
 int solve_pose(int d, const double* st, const double* Tk, double* Tout, double* loss_out);
@@ -295,8 +295,13 @@ struct gicp_ctx {
     double* d_dbg_det = nullptr;      // det(W) per source point (gicp_top_weights)
     size_t dbg_cap = 0;
     bool top_ready = false;           // the last pass recorded det(W)
+    // the top-k of that pass, computed inside the pass (same stream sync) for k = top_k_pref, the k the
+    // last gicp_top_weights call asked for: [0, 16) source, [16, 32) target indices, then 16 det values
+    int top_k_pref = 5, top_cached_k = 0;
+    int64_t* h_top = nullptr;         // pinned, 32 int64 + 16 double
     double* d_top_v = nullptr;        // top-k scratch: stage-1 candidates and outputs
-    int32_t* d_top_i = nullptr;
+    int64_t* d_top_i = nullptr;
+    int64_t* d_top_tgt = nullptr;     // [N] sorted order: target of each correspondence (with det(W))
     int64_t* d_top_out = nullptr;
     // per-source-tile candidate lists
     int32_t* d_list = nullptr;
@@ -868,6 +873,23 @@ void print_stamps(const unsigned long long* d_stamps, size_t nst) {
 }
 #endif
 
+// Top-k of the last pass's det(W) (k_top1 / k_top2) and its copy into the pinned c->h_top, enqueued on
+// the library's stream (the caller synchronises).
+void top_enqueue(gicp_ctx* c, int k) {
+    constexpr int kBlocks = 256;
+    if (!c->d_top_v) {
+        dalloc(c->d_top_v, (size_t)kBlocks * 16 + 16);
+        dalloc(c->d_top_i, (size_t)kBlocks * 16);
+        dalloc(c->d_top_out, 32);
+    }
+    if (!c->h_top) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_top), sizeof(int64_t) * 32 + sizeof(double) * 16));
+    double* ov = c->d_top_v + (size_t)kBlocks * 16;
+    HIPCHK(launch_top_weights(c->d_dbg_det, c->d_top_tgt, c->src.perm, c->src.n, k, c->d_top_v, c->d_top_i, kBlocks,
+                              ov, c->d_top_out, c->d_top_out + 16, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_top, c->d_top_out, sizeof(int64_t) * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_top + 32, ov, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
+}
+
 // One pass at pose T: statistics (all-reduced) into c->h_stats.
 void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
@@ -891,14 +913,16 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
             dalloc(c->d_dbg_w, n * 9);
             dalloc(c->d_dbg_dist, n);
             dalloc(c->d_dbg_det, n);
+            dalloc(c->d_top_tgt, n);
             c->dbg_cap = n;
         }
-        a.dbg_index = (dbg->index || dbg->want_top_weights) ? c->d_dbg_idx : nullptr;
+        a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
         a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
         a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
-        if (dbg->want_top_weights) {   // rows of other shards stay NaN (never selected)
-            HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * n, st));
+        if (dbg->want_top_weights) {   // rows of other shards stay NaN (never selected); one shard writes every row
+            if (c->nshards > 1) HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * n, st));
             a.dbg_det = c->d_dbg_det;
+            a.top_tgt = c->d_top_tgt;
         }
     }
     const int nsx = nstat_ext(d);
@@ -918,6 +942,11 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nsx, st));
     allreduce_stats(c);
     HIPCHK(hipMemcpyAsync(c->h_stats, c->d_state->stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, st));
+    c->top_cached_k = 0;
+    if (a.dbg_det && c->src.n > 0) {   // the top-k in the same stream sync as the pass
+        top_enqueue(c, c->top_k_pref);
+        c->top_cached_k = c->top_k_pref;
+    }
     if (dbg) {
         const size_t n = (size_t)c->src.n;
         if (dbg->index) HIPCHK(hipMemcpyAsync(dbg->index, c->d_dbg_idx, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
@@ -1036,6 +1065,7 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_dbg_w);
     dfree(c->d_dbg_dist);
     dfree(c->d_dbg_det);
+    dfree(c->d_top_tgt);
     dfree(c->d_cert_j);
     dfree(c->d_cert_gap);
     dfree(c->d_cert_pass);
@@ -1052,6 +1082,7 @@ void gicp_destroy(gicp_ctx* c) {
     c->next.release();
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_top) (void)hipHostFree(c->h_top);
     if (c->h_xchg) (void)hipHostFree(c->h_xchg);
     dfree(c->d_rot);
     for (auto& e : c->ev)
@@ -1212,23 +1243,15 @@ int gicp_top_weights(gicp_ctx* c, int k, int64_t* src_out, int64_t* tgt_out, dou
     if (!c || k < 1 || k > 16) return GICP_E_INVALID;
     return guard_impl(c, "gicp_top_weights", [&] {
         if (!c->top_ready) throw Fail{GICP_E_STATE, "no pass with want_top_weights since the last cloud change"};
-        constexpr int kBlocks = 256;
-        if (!c->d_top_v) {
-            dalloc(c->d_top_v, (size_t)kBlocks * 16 + 16);
-            dalloc(c->d_top_i, (size_t)kBlocks * 16);
-            dalloc(c->d_top_out, 32);
+        if (c->top_cached_k != k) {   // not computed with the pass: now (and for this k from the next pass on)
+            top_enqueue(c, k);
+            HIPCHK(hipStreamSynchronize(c->stream));
+            c->top_cached_k = c->top_k_pref = k;
         }
-        double* ov = c->d_top_v + (size_t)kBlocks * 16;
-        HIPCHK(launch_top_weights(c->d_dbg_det, c->d_dbg_idx, c->src.n, k, c->d_top_v, c->d_top_i, kBlocks, ov,
-                                  c->d_top_out, c->d_top_out + 16, c->stream));
-        std::vector<int64_t> hi(32);
-        std::vector<double> hv(16);
-        HIPCHK(hipMemcpyAsync(hi.data(), c->d_top_out, sizeof(int64_t) * 32, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(hv.data(), ov, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        const double* hv = reinterpret_cast<const double*>(c->h_top + 32);
         for (int r = 0; r < k; ++r) {
-            if (src_out) src_out[r] = hi[r];
-            if (tgt_out) tgt_out[r] = hi[16 + r];
+            if (src_out) src_out[r] = c->h_top[r];
+            if (tgt_out) tgt_out[r] = c->h_top[16 + r];
             if (det_out) det_out[r] = hv[r];
         }
     });

@@ -173,7 +173,8 @@ struct CorrArgs {
     int64_t* dbg_index;       // [N] original order (nullable)
     double* dbg_weight;       // [N][dim][dim] (nullable)
     double* dbg_dist;         // [N] (nullable)
-    double* dbg_det;          // [N] det(W), 0 if rejected, original order (nullable; gicp_top_weights)
+    double* dbg_det;          // [N] det(W), 0 if rejected, sorted order (nullable; gicp_top_weights)
+    int64_t* top_tgt;         // [N] with dbg_det, sorted order: original target index of the correspondence, -1 rejected
     int32_t cov_model;        // GICP_COV_* (include/gicp_hip.h)
     double pl_inv;            // 1 / (epsilon (1 - ratio)): n n^T = m m^T * pl_inv (point-to-plane)
     int32_t count_pairs;      // 1: accumulate evaluated pairs (diagnostic)

@@ -1922,7 +1922,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                          W[0][1] * (W[1][0] * W[2][2] - W[1][2] * W[2][0]) +
                          W[0][2] * (W[1][0] * W[2][1] - W[1][1] * W[2][0]);
             }
-            A.dbg_det[sc.perm[i]] = dt;
+            A.dbg_det[i] = dt;   // sorted order (coalesced); the top-k maps its winners through perm
+            A.top_tgt[i] = on ? (int64_t)tg.perm[j] : -1;
         }
         if (A.dbg_weight && q.valid) {
             double* o = A.dbg_weight + (int64_t)sc.perm[i] * D * D;
@@ -2465,7 +2466,7 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S) {
 // stable ascending argsort.  NaN (rows of other ranks' shards, memset 0xFF) never enters a list.
 constexpr int kTopMax = 16;
 
-__device__ __forceinline__ bool top_gt(double va, int32_t ia, double vb, int32_t ib) {
+__device__ __forceinline__ bool top_gt(double va, int64_t ia, double vb, int64_t ib) {
     return va > vb || (va == vb && ia > ib);
 }
 
@@ -2473,7 +2474,7 @@ __device__ __forceinline__ bool top_gt(double va, int32_t ia, double vb, int32_t
 // pops its k best with k rounds of a block-wide argmax over the threads' heads.
 struct TopList {
     double v[kTopMax];
-    int32_t i[kTopMax];
+    int64_t i[kTopMax];   // (original index << 32) | sorted position: ties order by the original index
     __device__ void init() {
 #pragma unroll
         for (int p = 0; p < kTopMax; ++p) {
@@ -2481,13 +2482,13 @@ struct TopList {
             i[p] = -1;
         }
     }
-    __device__ void insert(double cv, int32_t ci, int k) {
+    __device__ void insert(double cv, int64_t ci, int k) {
         if (!top_gt(cv, ci, -INFINITY, -1)) return;   // NaN / sentinel
 #pragma unroll
         for (int p = 0; p < kTopMax; ++p) {
             if (p < k && top_gt(cv, ci, v[p], i[p])) {
                 const double tv = v[p];
-                const int32_t ti = i[p];
+                const int64_t ti = i[p];
                 v[p] = cv;
                 i[p] = ci;
                 cv = tv;
@@ -2497,17 +2498,17 @@ struct TopList {
     }
 };
 
-__device__ void top_block_emit(TopList& L, int k, double* out_v, int32_t* out_i) {
+__device__ void top_block_emit(TopList& L, int k, double* out_v, int64_t* out_i) {
     __shared__ double s_v[4];
-    __shared__ int32_t s_i[4];
+    __shared__ int64_t s_i[4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int r = 0; r < k; ++r) {
         double bv = L.v[0];
-        int32_t bi = L.i[0];
+        int64_t bi = L.i[0];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const double ov = __shfl_xor(bv, off);
-            const int32_t oi = __shfl_xor(bi, off);
+            const int64_t oi = __shfl_xor(bi, off);
             if (top_gt(ov, oi, bv, bi)) {
                 bv = ov;
                 bi = oi;
@@ -2543,22 +2544,26 @@ __device__ void top_block_emit(TopList& L, int k, double* out_v, int32_t* out_i)
 }
 
 // stage 1: block b reduces its contiguous chunk of det[0, n) to k candidates
-__global__ void __launch_bounds__(256) k_top1(const double* __restrict__ det, int64_t n, int k, double* pv, int32_t* pi) {
+__global__ void __launch_bounds__(256) k_top1(const double* __restrict__ det, const int32_t* __restrict__ perm,
+                                              int64_t n, int k, double* pv, int64_t* pi) {
     const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
     const int64_t b0 = (int64_t)blockIdx.x * chunk, b1 = min(n, b0 + chunk);
     TopList L;
     L.init();
-    for (int64_t x = b0 + threadIdx.x; x < b1; x += blockDim.x) L.insert(det[x], (int32_t)x, k);
+    for (int64_t x = b0 + threadIdx.x; x < b1; x += blockDim.x)
+        L.insert(det[x], ((int64_t)perm[x] << 32) | (int64_t)x, k);
     top_block_emit(L, k, pv + (int64_t)blockIdx.x * k, pi + (int64_t)blockIdx.x * k);
 }
 
 // stage 2: one block merges the m = blocks x k candidates; ascending output (np.argsort(...)[-k:]),
 // plus the matched target index of each winner
-__global__ void __launch_bounds__(256) k_top2(const double* pv, const int32_t* pi, int m, int k,
-                                              const int64_t* __restrict__ tgt_index, double* ov, int64_t* osrc,
+// stage 2: one block reduces the stage-1 candidates; outputs ascending (np.argsort(det)[-k:] order), the
+// source as its original index, the target from the pass's sorted-order record (tgt_sorted)
+__global__ void __launch_bounds__(256) k_top2(const double* pv, const int64_t* pi, int m, int k,
+                                              const int64_t* __restrict__ tgt_sorted, double* ov, int64_t* osrc,
                                               int64_t* otgt) {
     __shared__ double s_ov[kTopMax];
-    __shared__ int32_t s_oi[kTopMax];
+    __shared__ int64_t s_oi[kTopMax];
     TopList L;
     L.init();
     for (int x = threadIdx.x; x < m; x += blockDim.x) L.insert(pv[x], pi[x], k);
@@ -2566,19 +2571,19 @@ __global__ void __launch_bounds__(256) k_top2(const double* pv, const int32_t* p
     __syncthreads();
     if ((int)threadIdx.x < k) {
         const int r = k - 1 - (int)threadIdx.x;   // descending -> ascending
-        const int32_t si = s_oi[r];
+        const int64_t si = s_oi[r];
         ov[threadIdx.x] = si >= 0 ? s_ov[r] : 0.0;
-        osrc[threadIdx.x] = si;
-        otgt[threadIdx.x] = si >= 0 ? tgt_index[si] : -1;
+        osrc[threadIdx.x] = si >= 0 ? (si >> 32) : -1;
+        otgt[threadIdx.x] = si >= 0 ? tgt_sorted[si & 0xFFFFFFFFll] : -1;
     }
 }
 
-hipError_t launch_top_weights(const double* det, const int64_t* tgt_index, int64_t n, int k, double* scratch_v,
-                              int32_t* scratch_i, int blocks, double* ov, int64_t* osrc, int64_t* otgt,
-                              hipStream_t st) {
+hipError_t launch_top_weights(const double* det, const int64_t* tgt_sorted, const int32_t* perm, int64_t n, int k,
+                              double* scratch_v, int64_t* scratch_i, int blocks, double* ov, int64_t* osrc,
+                              int64_t* otgt, hipStream_t st) {
     if (k < 1 || k > kTopMax || blocks < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_top1, dim3(blocks), dim3(256), 0, st, det, n, k, scratch_v, scratch_i);
-    hipLaunchKernelGGL(k_top2, dim3(1), dim3(256), 0, st, scratch_v, scratch_i, blocks * k, k, tgt_index, ov, osrc,
+    hipLaunchKernelGGL(k_top1, dim3(blocks), dim3(256), 0, st, det, perm, n, k, scratch_v, scratch_i);
+    hipLaunchKernelGGL(k_top2, dim3(1), dim3(256), 0, st, scratch_v, scratch_i, blocks * k, k, tgt_sorted, ov, osrc,
                        otgt);
     return hipGetLastError();
 }
