@@ -192,7 +192,9 @@ int gicp_pass_info(gicp_ctx* ctx, double out[GICP_PASS_INFO]);
  * them, ties broken towards the larger original index (the last k of a stable argsort).  Needs a
  * preceding gicp_iterate whose gicp_debug had want_top_weights = 1.  src_out[k]: original source
  * indices; tgt_out[k]: their matched target indices (-1 if rejected); det_out[k]: det(W).  Any
- * output may be NULL.  1 <= k <= 16; slots beyond the shard's point count are -1 / 0. */
+ * output may be NULL.  1 <= k <= 16; slots beyond the shard's point count are -1 / 0.  The pass
+ * itself computes the top-k for the k of the previous call (default 5), so that call returns without
+ * touching the device; another k costs one more launch and stream sync. */
 int gicp_top_weights(gicp_ctx* ctx, int k, int64_t* src_out, int64_t* tgt_out, double* det_out);
 
 /* Host solve of the inner problem (gicp.py:148-154): minimise
