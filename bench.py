@@ -3,19 +3,26 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n POINTS] [--dim 3]
 
 A step is one outer GICP iteration (gicp.py:116-167): correspondences + weights +
-statistics on the GPU (k_corr, reduced inside the launch), the RCCL all-reduce of the 77
-fp64 statistics when N > 1, and the pose solve + convergence test on the device (k_solve).
-Default workload = BASELINE.json
+statistics on the GPU (k_corr, reduced inside the launch), the RCCL all-reduce of the
+statistics when N > 1 (80 fp64 in 3-D = 74 statistics + 6 pass diagnostics; 32 = 26 + 6 in 2-D),
+and the pose solve + convergence test on the device (k_solve).  Default workload = BASELINE.json
 configs[2]: two synthetic 3-D clouds of 1M points, k = 20 covariances, d_c = 0.5 m,
 d_n = 1.0 m; with --gpus N the source is sharded over N ranks (configs[3]).
 Convergence is disabled so every run does exactly K iterations.
+
+Ranks: under a launcher (torch.distributed.run sets WORLD_SIZE) every process is one rank and
+--gpus must equal WORLD_SIZE.  Without one, --gpus N > 1 starts N rank processes itself -- as
+children (python -m torch.distributed.run --nproc-per-node N ... bench.py ...), before anything
+touches the GPU -- forwards rank 0's line and exits with the launcher's status; with fewer than N
+GPUs visible it exits non-zero naming the count (never a silent 1-GPU run).  --dry-run starts the
+ranks on the CPU (gloo) and only reports the rank plumbing.
 
 The timed registration starts COLD: the engine's pose-dependent caches (candidate lists,
 nearest-neighbour certificates, last matches) are dropped after the warmup (gicp_reset_cache), so
 the K iterations pay the first full walks from the identity exactly as a fresh registration does.
 roofline.achieved follows SURVEY.md §8(d): algorithmic bytes per k_corr launch
-B = 24 (N/G + M) (fp32 xyz + fp32 normal of every source point of the shard and every target
-point, read once) over the HIP-event mean k_corr duration.
+B = 8 dim (N/G + M) (fp32 xyz + fp32 normal of every source point of the shard and every target
+point, read once: 24 B in 3-D, 16 B in 2-D) over the HIP-event mean k_corr duration.
 """
 import argparse
 import json
@@ -32,9 +39,22 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md, HBM3E peak
 FP32_PEAK_TFLOPS = 157.3     # MI355X vector FP32 peak
-BYTES_PER_POINT = 24         # SURVEY.md §8(d) contract: fp32 xyz (12) + fp32 unit normal (12), read once
 IMPL_BYTES_PER_POINT = 80    # DESIGN.md §3 layout actually read: fp32 screen (16) + fp64 xyz (32) + covariance (32)
 FLOP_PER_PAIR = 8            # 3 sub + 1 mul + 2 fma (counted as 2) in the fp32 screen
+# gicp.py itself (2-D only), timed in the build container on 1 core: context for
+# cpu_baseline, never the comparator (the reference cannot travel to the GPU box)
+GICP_PY_IT_S = {100_000: 0.062, 1_000_000: 0.0063}
+
+
+def bytes_per_point(dim):
+    """SURVEY.md §8(d) contract: fp32 coordinates + fp32 unit normal, read once (24 B 3-D, 16 B 2-D)."""
+    return 8 * dim
+
+
+def stats_exchanged(dim):
+    """fp64 values the per-iteration all-reduce carries: the statistics + GICP_PASS_INFO diagnostics."""
+    ns = dim * (dim + 1) // 2
+    return ns * ns + ns * dim + ns + dim * dim + dim + 2 + 6
 
 
 def parse():
@@ -53,7 +73,51 @@ def parse():
                     help="diagnostic: one process runs only shard 0 of S (no collective) to time a rank of an "
                          "S-GPU job; the line is marked and is not the metric")
     ap.add_argument("--shard-index", type=int, default=0, help="diagnostic: which shard --shard-sim runs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks (gloo, CPU only) and report RANK / WORLD_SIZE; no GPU work")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """--gpus N > 1 without a launcher: N rank processes under torch.distributed.run, as CHILD
+    processes (never exec: nothing here has touched the GPU, and nothing may before the ranks do).
+    Returns the exit status to leave with."""
+    if not a.dry_run:
+        import torch
+        ngpu = torch.cuda.device_count()   # counts devices without initialising HIP on this image
+        if ngpu < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs, but {ngpu} GPU(s) are visible; "
+                  "refusing to run (no fallback to fewer GPUs)", file=sys.stderr)
+            return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC: RCCL's only mode on this driver
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(world, rank, local):
+    """Rank plumbing only (CPU, gloo): every rank reports itself, rank 0 prints the gathered list."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "local_rank": local, "world_size": world})
+        dist.destroy_process_group()
+    else:
+        got = [{"rank": rank, "local_rank": local, "world_size": world}]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world_size": world, "ranks": got}))
 
 
 def workload(n, dim):
@@ -109,9 +173,20 @@ def cpu_baseline(src, tgt, kw, workers, iters=1):
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks; refusing",
+              file=sys.stderr)
+        sys.exit(2)
+    if a.dry_run:
+        dry_run(world, rank, local)
+        return
     dist = None
     if world > 1:
         import torch
@@ -129,6 +204,9 @@ def main():
         uid = [gicp.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
+    comm_ranks, _, comm_kind = eng.comm_ranks()
+    if world > 1 and (comm_ranks != world or comm_kind != "rccl"):
+        raise SystemExit(f"rank {rank}: the RCCL communicator reports {comm_ranks} ranks ({comm_kind}), expected {world}")
     t0 = time.perf_counter()
     eng.set_target(tgt, params)
     if world == 1 and a.shard_sim > 1:
@@ -201,7 +279,7 @@ def main():
     rot_err, tr_err = rotation_angle_error(T, Tgt), translation_error(T, Tgt)
     n_shard = a.n / max(world, a.shard_sim)
     corr_avg_ms = corr_ms_total / a.steps
-    alg_bytes = BYTES_PER_POINT * (n_shard + a.n)
+    alg_bytes = bytes_per_point(a.dim) * (n_shard + a.n)
     impl_bytes = IMPL_BYTES_PER_POINT * (n_shard + a.n)
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
     n_mov = min(10, a.steps)
@@ -223,11 +301,14 @@ def main():
                  else "synthetic (2-D segment scene of BASELINE.md §3, 0.5 px noise)"),
         "config": {"workload": name, "n_source": a.n, "n_target": a.n, "dim": a.dim,
                    "k": 20 if a.dim == 3 else 6, **kw,
-                   "parallelism": f"dp{world} (source shards; RCCL all-reduce of 74 fp64 per iteration)"},
+                   "parallelism": f"dp{world} (source shards; RCCL all-reduce of {stats_exchanged(a.dim)} fp64 "
+                                  f"per iteration)" if world > 1 else "dp1 (one GPU, no collective)"},
+        "comm_ranks": comm_ranks,
+        "comm": comm_kind,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_corr", "kernel_avg_ms": corr_avg_ms, "alg_bytes_per_launch": alg_bytes,
-                     "alg_bytes_rule": "SURVEY.md 8(d): 24 B x (N/G + M)",
+                     "alg_bytes_rule": f"SURVEY.md 8(d): {bytes_per_point(a.dim)} B x (N/G + M)",
                      "impl_bytes_per_launch": impl_bytes,
                      "impl_frac": impl_bytes / (corr_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_timing": "HIP events, every k_corr launch of K timed once (8 identical cold-start "
@@ -264,6 +345,12 @@ def main():
                                               f"the same {name} clouds, 1 outer iteration after {setup:.1f} s "
                                               f"setup (covariances), {dt:.1f} s timed; parity of the 3-D oracle is "
                                               f"pinned by its 2-D instance (reference fixtures) + ground truth"}
+            ref = GICP_PY_IT_S.get(a.n)
+            line["cpu_baseline"]["reference_gicp_py"] = {
+                "value": ref, "unit": "it/s", "cores": 1, "dim": 2,
+                "note": ("context only: gicp.py itself (2-D only, 3-D raises) on 2-D segment clouds of the same N, "
+                         "1 core of the build container's 8-core Xeon, BASELINE.md §3; the reference cannot run on "
+                         "the GPU box") if ref else "no gicp.py timing at this N (BASELINE.md §3: 100k, 1M)"}
         except Exception as e:  # the baseline must never hide the GPU line
             line["cpu_baseline"] = {"value": None, "error": repr(e)}
     else:

@@ -1121,6 +1121,26 @@ int gicp_comm_init(gicp_ctx* c, int nranks, int rank, const char id[GICP_COMM_ID
     });
 }
 
+int gicp_comm_ranks(gicp_ctx* c, int* nranks, int* rank, int* kind) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_comm_ranks", [&] {
+        int n = 1, r = 0, k = 0;
+        if (c->comm) {
+            ncclResult_t e = ncclCommCount(c->comm, &n);
+            if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);
+            if (e != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(e)};
+            k = 1;
+        } else if (c->hook) {
+            n = c->nranks;
+            r = c->rank;
+            k = 2;
+        }
+        if (nranks) *nranks = n;
+        if (rank) *rank = r;
+        if (kind) *kind = k;
+    });
+}
+
 int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_set_target", [&] {

@@ -135,6 +135,13 @@ class Engine:
     def comm_init(self, nranks, rank, uid: bytes):
         check(self._lib.gicp_comm_init(self._ctx, nranks, rank, uid), self._ctx, "gicp_comm_init")
 
+    def comm_ranks(self):
+        """(nranks, rank, kind) of the statistics exchange, read back from the RCCL communicator
+        (gicp_comm_ranks); kind is 'none', 'rccl' or 'hook'."""
+        n, r, k = C.c_int(), C.c_int(), C.c_int()
+        check(self._lib.gicp_comm_ranks(self._ctx, C.byref(n), C.byref(r), C.byref(k)), self._ctx, "gicp_comm_ranks")
+        return n.value, r.value, {0: "none", 1: "rccl", 2: "hook"}[k.value]
+
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = C.create_string_buffer(_lib.COMM_ID_BYTES)

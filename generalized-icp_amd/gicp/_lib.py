@@ -99,6 +99,7 @@ SIGNATURES = {
     "gicp_last_error": (C.c_char_p, [_VP]),
     "gicp_comm_unique_id": (C.c_int, [C.c_char_p]),
     "gicp_comm_init": (C.c_int, [_VP, C.c_int, C.c_int, C.c_char_p]),
+    "gicp_comm_ranks": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "gicp_set_target": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params)]),
     "gicp_set_source": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params), C.c_int, C.c_int]),
     "gicp_target_to_source": (C.c_int, [_VP, C.c_int, C.c_int]),

@@ -132,6 +132,11 @@ const char* gicp_last_error(const gicp_ctx* ctx);
 /* ---- multi-GPU: one process per GPU, RCCL over xGMI ---------------------- */
 int gicp_comm_unique_id(char out[GICP_COMM_ID_BYTES]);   /* rank 0, then broadcast out-of-band */
 int gicp_comm_init(gicp_ctx* ctx, int nranks, int rank, const char id[GICP_COMM_ID_BYTES]);
+/* The exchange this context's statistics go through, read back from the communicator itself
+ * (ncclCommCount / ncclCommUserRank): *nranks = 1 and *rank = 0 without one; with a host hook
+ * (gicp_set_allreduce) the values gicp_comm_init was last given, else 1 / 0.  *kind: 0 none,
+ * 1 RCCL, 2 host hook.  Any output may be NULL. */
+int gicp_comm_ranks(gicp_ctx* ctx, int* nranks, int* rank, int* kind);
 
 /* ---- clouds -------------------------------------------------------------- */
 /* Target cloud (gicp.py:101,104): builds the tile index and the per-point

@@ -1,0 +1,65 @@
+"""bench.py's rank launcher (the driver runs `python bench.py --gpus N`, and also
+`torch.distributed.run ... bench.py --gpus N`): N > 1 without a launcher starts N child ranks,
+a mismatch with WORLD_SIZE is refused, too few GPUs is an error naming the count.  CPU only."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH, *args], env=env, capture_output=True, text=True, timeout=timeout,
+                          cwd=ROOT)
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_dry_run_spawns_two_ranks():
+    r = _run(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    d = _json_line(r.stdout)
+    assert d["dry_run"] and d["world_size"] == 2
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1]
+    assert sorted(x["local_rank"] for x in d["ranks"]) == [0, 1]
+    assert all(x["world_size"] == 2 for x in d["ranks"])
+
+
+def test_dry_run_one_rank_needs_no_launcher():
+    r = _run(["--gpus", "1", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    d = _json_line(r.stdout)
+    assert d["world_size"] == 1 and d["ranks"] == [{"rank": 0, "local_rank": 0, "world_size": 1}]
+
+
+def test_too_few_gpus_is_an_error_naming_the_count():
+    import torch
+    have = torch.cuda.device_count()
+    want = have + 1
+    if want < 2:
+        want = 2
+    r = _run(["--gpus", str(want), "--steps", "1"])
+    assert r.returncode != 0
+    assert f"{have} GPU(s) are visible" in r.stderr and f"--gpus {want}" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")], "no bench line on a refused run"
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "3", "--dry-run"], env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.parametrize("bad", ["0", "-1"])
+def test_gpus_must_be_positive(bad):
+    r = _run(["--gpus", bad, "--dry-run"])
+    assert r.returncode != 0
