@@ -35,7 +35,7 @@ hipError_t launch_build_tiles(const double*, int, int32_t*, TileInfo*, int, doub
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
 hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
-hipError_t launch_solve(IterState*, int, hipStream_t);
+hipError_t launch_solve(IterState*, int, hipStream_t, double*);
 hipError_t launch_graph(const GraphArgs&, int, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
@@ -347,6 +347,13 @@ struct gicp_ctx {
     std::vector<float> iter_ms;       // sampled k_corr time per iteration of the last align (-1: not sampled)
     double* d_rot = nullptr;          // gicp_rotated_covariances output
     size_t cap_rot = 0;
+    // gicp_align_trace: per-iteration rows recorded on the device ([iter][(d+1)^2 + 1] pose + loss;
+    // top-k rows [iter][16] source, target, det), copied out once after the loop
+    double* d_hist = nullptr;
+    size_t cap_hist = 0;
+    int64_t* d_trace_top = nullptr;   // [iter][16] source, then [iter][16] target
+    double* d_trace_det = nullptr;    // [iter][16]
+    size_t cap_ttop = 0, cap_tdet = 0;
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
     // diagnostics of the last pass
@@ -873,18 +880,36 @@ void print_stamps(const unsigned long long* d_stamps, size_t nst) {
 }
 #endif
 
+// per-point debug outputs of a pass (gicp_debug) and the det(W) record of the top-k, grow-only
+void ensure_dbg(gicp_ctx* c) {
+    const size_t n = (size_t)c->src.n;
+    if (c->dbg_cap < n) {
+        dalloc(c->d_dbg_idx, n);
+        dalloc(c->d_dbg_w, n * 9);
+        dalloc(c->d_dbg_dist, n);
+        dalloc(c->d_dbg_det, n);
+        dalloc(c->d_top_tgt, n);
+        c->dbg_cap = n;
+    }
+}
+
+constexpr int kTopBlocks = 256;   // stage-1 blocks of the top-k of det(W)
+
+void ensure_top_scratch(gicp_ctx* c) {
+    if (!c->d_top_v) {
+        dalloc(c->d_top_v, (size_t)kTopBlocks * 16 + 16);
+        dalloc(c->d_top_i, (size_t)kTopBlocks * 16);
+        dalloc(c->d_top_out, 32);
+    }
+}
+
 // Top-k of the last pass's det(W) (k_top1 / k_top2) and its copy into the pinned c->h_top, enqueued on
 // the library's stream (the caller synchronises).
 void top_enqueue(gicp_ctx* c, int k) {
-    constexpr int kBlocks = 256;
-    if (!c->d_top_v) {
-        dalloc(c->d_top_v, (size_t)kBlocks * 16 + 16);
-        dalloc(c->d_top_i, (size_t)kBlocks * 16);
-        dalloc(c->d_top_out, 32);
-    }
+    ensure_top_scratch(c);
     if (!c->h_top) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_top), sizeof(int64_t) * 32 + sizeof(double) * 16));
-    double* ov = c->d_top_v + (size_t)kBlocks * 16;
-    HIPCHK(launch_top_weights(c->d_dbg_det, c->d_top_tgt, c->src.perm, c->src.n, k, c->d_top_v, c->d_top_i, kBlocks,
+    double* ov = c->d_top_v + (size_t)kTopBlocks * 16;
+    HIPCHK(launch_top_weights(c->d_dbg_det, c->d_top_tgt, c->src.perm, c->src.n, k, c->d_top_v, c->d_top_i, kTopBlocks,
                               ov, c->d_top_out, c->d_top_out + 16, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_top, c->d_top_out, sizeof(int64_t) * 32, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_top + 32, ov, sizeof(double) * 16, hipMemcpyDeviceToHost, c->stream));
@@ -907,20 +932,12 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     CorrArgs a = corr_args(c, 1);
     c->top_ready = false;
     if (dbg && (dbg->index || dbg->weight || dbg->distance || dbg->want_top_weights)) {
-        const size_t n = (size_t)c->src.n;
-        if (c->dbg_cap < n) {
-            dalloc(c->d_dbg_idx, n);
-            dalloc(c->d_dbg_w, n * 9);
-            dalloc(c->d_dbg_dist, n);
-            dalloc(c->d_dbg_det, n);
-            dalloc(c->d_top_tgt, n);
-            c->dbg_cap = n;
-        }
+        ensure_dbg(c);
         a.dbg_index = dbg->index ? c->d_dbg_idx : nullptr;
         a.dbg_weight = dbg->weight ? c->d_dbg_w : nullptr;
         a.dbg_dist = dbg->distance ? c->d_dbg_dist : nullptr;
         if (dbg->want_top_weights) {   // rows of other shards stay NaN (never selected); one shard writes every row
-            if (c->nshards > 1) HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * n, st));
+            if (c->nshards > 1) HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * c->src.n, st));
             a.dbg_det = c->d_dbg_det;
             a.top_tgt = c->d_top_tgt;
         }
@@ -1085,6 +1102,9 @@ void gicp_destroy(gicp_ctx* c) {
     if (c->h_top) (void)hipHostFree(c->h_top);
     if (c->h_xchg) (void)hipHostFree(c->h_xchg);
     dfree(c->d_rot);
+    dfree(c->d_hist);
+    dfree(c->d_trace_top);
+    dfree(c->d_trace_det);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1287,6 +1307,11 @@ int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_o
 }
 
 int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_out, gicp_result* res) {
+    return gicp_align_trace(c, T0, p, T_out, res, nullptr);
+}
+
+int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_out, gicp_result* res,
+                     gicp_trace* trace) {
     if (!c || !T_out) return GICP_E_INVALID;
     return guard_impl(c, "gicp_align", [&] {
         if (!c->tgt.n || !c->src.n) throw Fail{GICP_E_STATE, "set_target and set_source first"};
@@ -1297,6 +1322,25 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         c->psrc.cov_model = prm.cov_model;
         ensure_workspace(c);
         hipStream_t st = c->stream;
+        // per-iteration trace rows (gicp_trace): pose + loss from k_solve, top-k rows after k_corr
+        const int HS = n1 * n1 + 1;
+        const int tk = trace ? trace->top_k : 0;
+        if (trace) {
+            if (trace->capacity < std::max(0, prm.max_iterations))
+                throw Fail{GICP_E_INVALID, "gicp_trace.capacity < max_iterations"};
+            if (tk < 0 || tk > 16) throw Fail{GICP_E_INVALID, "gicp_trace.top_k must be 0..16"};
+            const size_t rows = (size_t)std::max(1, prm.max_iterations);
+            dreserve(c->d_hist, c->cap_hist, rows * HS);
+            if (tk > 0) {
+                ensure_dbg(c);
+                ensure_top_scratch(c);
+                dreserve(c->d_trace_top, c->cap_ttop, rows * 32);
+                dreserve(c->d_trace_det, c->cap_tdet, rows * 16);
+                // rows of other shards stay NaN (never selected); one shard writes every row
+                if (c->nshards > 1) HIPCHK(hipMemsetAsync(c->d_dbg_det, 0xFF, sizeof(double) * c->src.n, st));
+            }
+        }
+        c->top_ready = false;
         // device state: T0, last_loss = inf (gicp.py:106-110)
         IterState& hs = *c->h_state;
         std::memset(&hs, 0, offsetof(IterState, stats));
@@ -1333,15 +1377,25 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
             const int B = std::min(prm.max_iterations - enq,
                                    c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 8);
             for (int b = 0; b < B; ++b) {
+                const int it = enq + b;
                 CorrArgs a = corr_args(c, 0);
-                if (enq + b < c->moving_iters) a.unit_map = c->moving_map;
-                const bool ev = timing && (enq + b) % kEvStride == kEvOffset;
+                if (it < c->moving_iters) a.unit_map = c->moving_map;
+                if (tk > 0) {   // det(W) of every point, for this iteration's top-k rows (gicp.py:170)
+                    a.dbg_det = c->d_dbg_det;
+                    a.top_tgt = c->d_top_tgt;
+                }
+                const bool ev = timing && it % kEvStride == kEvOffset;
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b], st));
                 if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
                 else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nstat_ext(d), st));
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b + 1], st));
+                if (tk > 0)   // launched after convergence too (the pass exited at once): rows >= iter are ignored
+                    HIPCHK(launch_top_weights(c->d_dbg_det, c->d_top_tgt, c->src.perm, c->src.n, tk, c->d_top_v,
+                                              c->d_top_i, kTopBlocks, c->d_trace_det + (size_t)it * 16,
+                                              c->d_trace_top + (size_t)it * 32, c->d_trace_top + (size_t)it * 32 + 16,
+                                              st));
                 allreduce_stats(c);
-                HIPCHK(launch_solve(c->d_state, d, st));
+                HIPCHK(launch_solve(c->d_state, d, st, trace ? c->d_hist + (size_t)it * HS : nullptr));
             }
             enq += B;
             HIPCHK(hipMemcpyAsync(&hs, c->d_state, sizeof(IterState), hipMemcpyDeviceToHost, st));
@@ -1360,6 +1414,29 @@ int gicp_align(gicp_ctx* c, const double* T0, const gicp_params* p, double* T_ou
         }
         const auto t1 = std::chrono::steady_clock::now();
         c->iter_ms.resize((size_t)std::max(0, std::min(hs.iter, prm.max_iterations)));
+        if (trace && hs.iter > 0) {   // the rows of the iterations executed, in one copy per array
+            const int ni = std::min(hs.iter, prm.max_iterations);
+            std::vector<double> hist((size_t)ni * HS);
+            HIPCHK(hipMemcpyAsync(hist.data(), c->d_hist, sizeof(double) * hist.size(), hipMemcpyDeviceToHost, st));
+            std::vector<int64_t> ttop;
+            std::vector<double> tdet;
+            if (tk > 0) {
+                ttop.resize((size_t)ni * 32);
+                tdet.resize((size_t)ni * 16);
+                HIPCHK(hipMemcpyAsync(ttop.data(), c->d_trace_top, sizeof(int64_t) * ttop.size(), hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(tdet.data(), c->d_trace_det, sizeof(double) * tdet.size(), hipMemcpyDeviceToHost, st));
+            }
+            HIPCHK(hipStreamSynchronize(st));
+            for (int k = 0; k < ni; ++k) {
+                if (trace->poses) std::memcpy(trace->poses + (size_t)k * n1 * n1, &hist[(size_t)k * HS], sizeof(double) * n1 * n1);
+                if (trace->losses) trace->losses[k] = hist[(size_t)k * HS + n1 * n1];
+                for (int r = 0; r < tk; ++r) {
+                    if (trace->top_src) trace->top_src[(size_t)k * tk + r] = ttop[(size_t)k * 32 + r];
+                    if (trace->top_tgt) trace->top_tgt[(size_t)k * tk + r] = ttop[(size_t)k * 32 + 16 + r];
+                    if (trace->top_det) trace->top_det[(size_t)k * tk + r] = tdet[(size_t)k * 16 + r];
+                }
+            }
+        }
         if (hs.solve_fail) throw Fail{GICP_E_INVALID, "pose solve failed (degenerate statistics)"};
         std::memcpy(T_out, hs.T, sizeof(double) * n1 * n1);
         if (res) {

@@ -2373,7 +2373,7 @@ __device__ __forceinline__ SolveOut<D> solve_pose_wave(const double* st, const d
 // 0-63); `sync` orders that wave's LDS traffic.  `Ls` is an LDS copy of the device state S (header
 // and statistics, loaded in one round trip): everything is read from it, only the results go to S.
 template <int D, class Sync>
-__device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl, Sync sync) {
+__device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl, Sync sync, double* hist) {
     const int lane = threadIdx.x & 63;
     constexpr int NSX = nstat_ext(D);
     const double* st = Ls->stats;
@@ -2383,6 +2383,12 @@ __device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl,
     if (lane != 0) return;
     const IterState* SR = Ls;   // the state as this launch found it
     const int it = SR->iter;
+    if (hist) {   // gicp_trace row of this iteration: the pose its pass ran at, then min_loss
+        constexpr int NT = (D + 1) * (D + 1);
+#pragma unroll
+        for (int k = 0; k < NT; ++k) hist[k] = SR->T[k];
+        hist[NT] = r.loss;
+    }
     S->iter = it + 1;
     if (!r.ok) S->solve_fail = 1;
     S->loss = r.loss;
@@ -2438,7 +2444,7 @@ __device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl,
 // round trip -- the statistics were just written by k_corr's last workgroup, likely on another XCD, so
 // each dependent global read costs a full memory latency; every later read is an LDS read.
 template <int D>
-__global__ void __launch_bounds__(64) k_solve(IterState* S) {
+__global__ void __launch_bounds__(64) k_solve(IterState* S, double* hist) {
     constexpr int NLOAD = (int)(offsetof(IterState, stats) / sizeof(double)) + nstat_ext(D);
     static_assert(NLOAD <= 128, "state header + statistics: two loads per lane");
     __shared__ IterState s_state;
@@ -2455,7 +2461,7 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S) {
     __syncthreads();
     GICP_SOLVE_STAMP(1);
     if (s_state.converged) return;
-    solve_update<D>(S, &s_state, s_sl, [] { __syncthreads(); });
+    solve_update<D>(S, &s_state, s_sl, [] { __syncthreads(); }, hist);
     GICP_SOLVE_STAMP(13);
 }
 
@@ -2700,9 +2706,9 @@ hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_solve(IterState* st, int dim, hipStream_t stream) {
-    if (dim == 2) hipLaunchKernelGGL(k_solve<2>, dim3(1), dim3(64), 0, stream, st);
-    else hipLaunchKernelGGL(k_solve<3>, dim3(1), dim3(64), 0, stream, st);
+hipError_t launch_solve(IterState* st, int dim, hipStream_t stream, double* hist) {
+    if (dim == 2) hipLaunchKernelGGL(k_solve<2>, dim3(1), dim3(64), 0, stream, st, hist);
+    else hipLaunchKernelGGL(k_solve<3>, dim3(1), dim3(64), 0, stream, st, hist);
     return hipGetLastError();
 }
 

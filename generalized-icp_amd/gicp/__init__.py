@@ -19,7 +19,7 @@ from collections.abc import Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import Debug, Params, Result, check, dptr
+from ._lib import Debug, Params, Result, Trace, check, dptr
 
 __all__ = ["gicp", "apply_transformation", "Engine", "RotatedCovariances", "expand_stats", "stats_size",
            "default_params"]
@@ -105,6 +105,8 @@ class Engine:
         self._lib = _lib.load()
         self._ctx = C.c_void_p()
         rc = self._lib.gicp_create(C.byref(self._ctx), int(device))
+        if rc == _lib.GICP_E_INVALID:
+            raise ValueError(f"gicp_create(device={device}): no such GPU")
         if rc != _lib.GICP_OK:
             raise _lib.GicpError(rc, f"gicp_create(device={device}): {self._lib.gicp_strerror(rc).decode()}")
         self.device = device
@@ -301,20 +303,42 @@ class Engine:
               self._ctx, "gicp_top_weights")
         return st, si, ti, dt
 
-    def align(self, T0=None, params=None):
-        """The whole outer loop (gicp.py:116-167) natively; returns (T, result dict)."""
+    def align(self, T0=None, params=None, trace=False, top_k=0):
+        """The whole outer loop (gicp.py:116-167) natively; returns (T, result dict), plus with
+        trace=True a dict of per-iteration rows recorded on the device (gicp_align_trace): 'poses'
+        [iters, d+1, d+1] (the pose each pass ran at), 'losses' [iters], and with top_k > 0 the
+        pass's top_k largest det(W): 'top_src', 'top_tgt' [iters, top_k] original indices, 'top_det'."""
         d = self.dim
         T0 = np.eye(d + 1) if T0 is None else np.ascontiguousarray(np.asarray(T0, dtype=np.float64))
         Tout = np.empty((d + 1, d + 1))
         res = Result()
         p = params or default_params(d)
-        check(self._lib.gicp_align(self._ctx, dptr(T0), C.byref(p), dptr(Tout), C.byref(res)), self._ctx,
-              "gicp_align")
+        if trace:
+            cap = max(1, int(p.max_iterations))
+            rows = dict(poses=np.zeros((cap, d + 1, d + 1)), losses=np.zeros(cap),
+                        top_src=np.full((cap, max(top_k, 1)), -1, dtype=np.int64),
+                        top_tgt=np.full((cap, max(top_k, 1)), -1, dtype=np.int64),
+                        top_det=np.zeros((cap, max(top_k, 1))))
+            p64 = C.POINTER(C.c_int64)
+            tr = Trace(cap, int(top_k), dptr(rows["poses"]), dptr(rows["losses"]),
+                       rows["top_src"].ctypes.data_as(p64), rows["top_tgt"].ctypes.data_as(p64), dptr(rows["top_det"]))
+            check(self._lib.gicp_align_trace(self._ctx, dptr(T0), C.byref(p), dptr(Tout), C.byref(res), C.byref(tr)),
+                  self._ctx, "gicp_align_trace")
+        else:
+            check(self._lib.gicp_align(self._ctx, dptr(T0), C.byref(p), dptr(Tout), C.byref(res)), self._ctx,
+                  "gicp_align")
         r = res.as_dict()
         r.pop("pad", None)
         r.pop("pad2", None)
         r["stop_reason"] = _lib.STOP_REASONS.get(r["stop_reason"], r["stop_reason"])
-        return Tout, r
+        if not trace:
+            return Tout, r
+        n = min(int(r["iterations"]), int(p.max_iterations))
+        out = {k: v[:n] for k, v in rows.items()}
+        if not top_k:
+            for k in ("top_src", "top_tgt", "top_det"):
+                out.pop(k)
+        return Tout, r, out
 
 
 def solve_pose(stats, T_k):
@@ -391,16 +415,21 @@ FAITHFUL_MAX_POINTS = 5000
 
 class RotatedCovariances(Sequence):
     """all_source_cov_matrices of the fast path (gicp.py:120-121,174), held lazily: element k is
-    R_k C_s,i R_kᵀ for every source point, R_k the rotation of iteration k.  Only the rotations are
-    stored; an element is computed when read -- on the device (gicp_rotated_covariances) while the
-    engine still holds this source cloud, else from the initial covariances on the host (same
-    formula, R C Rᵀ per point).  Behaves as the reference's list for len / indexing / iteration."""
+    R_k C_s,i R_kᵀ for every source point (rigid invariance), R_k the rotation of
+    iteration k.  Only the initial covariances and the rotations are stored; an element is computed
+    on the host when read (always the same formula, so a re-read is bit-identical whatever the engine
+    did meanwhile), and the last two elements read are kept, so the reference's per-point access
+    `all_source_cov_matrices[step][i]` (visualization.py:158) costs one computation per step.  Holds no
+    engine: picklable (e.g. through the multiprocessing Queue of robot-visualization.py:153,166).
+    Behaves as the reference's list for len / indexing / iteration."""
 
-    def __init__(self, engine, init_cov):
-        self._eng = engine
-        self._gen = engine.generation
+    _CACHE = 2
+
+    def __init__(self, init_cov, rotations=()):
         self._init = init_cov
-        self._R = []
+        self._R = [np.array(R, dtype=np.float64) for R in rotations]
+        self._cache = {}
+        self.computed = 0   # elements materialised so far (a test bounds it)
 
     def append_rotation(self, R):
         self._R.append(np.array(R, dtype=np.float64))
@@ -408,16 +437,32 @@ class RotatedCovariances(Sequence):
     def __len__(self):
         return len(self._R)
 
-    def _one(self, R):
-        e = self._eng
-        if e is not None and e._ctx and e.generation == self._gen:
-            return e.rotated_covariances(R, "source")
-        return np.einsum("ab,nbc,dc->nad", R, self._init, R)
+    def _one(self, k):
+        hit = self._cache.get(k)
+        if hit is not None:
+            return hit
+        R = self._R[k]
+        out = np.matmul(np.matmul(R, self._init), R.T)
+        self.computed += 1
+        if len(self._cache) >= self._CACHE:
+            self._cache.pop(next(iter(self._cache)))
+        self._cache[k] = out
+        return out
 
     def __getitem__(self, k):
         if isinstance(k, slice):
-            return [self._one(R) for R in self._R[k]]
-        return self._one(self._R[k])
+            return [self._one(i) for i in range(len(self._R))[k]]
+        k = range(len(self._R))[k]   # negative indices, IndexError as a list
+        return self._one(k)
+
+    def __getstate__(self):
+        return {"init": self._init, "R": self._R}
+
+    def __setstate__(self, st):
+        self._init = st["init"]
+        self._R = st["R"]
+        self._cache = {}
+        self.computed = 0
 
     def __repr__(self):
         return f"RotatedCovariances({len(self)} iterations x {len(self._init)} points)"
@@ -428,6 +473,65 @@ def _engine(device):
     if eng is None:
         eng = _ENGINES[device] = Engine(device)
     return eng
+
+
+def _devices(device, devices):
+    """The GPUs a gicp() call runs on: [device], or the distinct entries of `devices`."""
+    if devices is None:
+        return [int(device)]
+    devs = [int(x) for x in devices]
+    if not devs:
+        raise ValueError("devices must name at least one GPU")
+    if len(set(devs)) != len(devs):
+        raise ValueError(f"devices lists a GPU more than once: {devs}")
+    return devs
+
+
+class _ThreadSum:
+    """Statistics exchange of a multi-device gicp() call (one host thread per GPU): every rank's
+    buffer in, the sum in rank order out -- the same bits on every rank, so every device's solve and
+    convergence test agree.  A failing rank aborts the barrier and the others raise instead of waiting."""
+
+    def __init__(self, world, timeout=300.0):
+        import threading
+        self.world = world
+        self.slots = [None] * world
+        self.bar = threading.Barrier(world, timeout=timeout)
+
+    def __call__(self, rank, buf):
+        self.slots[rank] = np.array(buf, dtype=np.float64)
+        self.bar.wait()
+        total = self.slots[0].copy()
+        for r in range(1, self.world):
+            total += self.slots[r]
+        self.bar.wait()
+        return total
+
+    def abort(self):
+        self.bar.abort()
+
+
+def _run_ranks(engines, fn):
+    """fn(rank, engine) on one thread per engine (ctypes releases the GIL inside the library);
+    returns the results in rank order, re-raising the first failure."""
+    if len(engines) == 1:
+        return [fn(0, engines[0])]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(engines)) as ex:
+        futs = [ex.submit(fn, r, e) for r, e in enumerate(engines)]
+        return [f.result() for f in futs]
+
+
+def _merge_top(rows, k=5):
+    """The k largest det(W) over the ranks' top-k rows, ascending as np.argsort(det)[-k:] orders them
+    (equal dets: larger original index last).  rows: [(src, tgt, det), ...] per rank."""
+    src = np.concatenate([r[0] for r in rows])
+    tgt = np.concatenate([r[1] for r in rows])
+    det = np.concatenate([r[2] for r in rows])
+    ok = src >= 0
+    src, tgt, det = src[ok], tgt[ok], det[ok]
+    order = np.lexsort((src, det))[-k:]
+    return src[order], tgt[order], det[order]
 
 
 def pcl_stop(T_old, T_new, mse, prev_mse, transformation_epsilon=0.0, rotation_epsilon=0.0,
@@ -455,8 +559,8 @@ def pcl_stop(T_old, T_new, mse, prev_mse, transformation_epsilon=0.0, rotation_e
 
 def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
          max_distance_nearest_neighbors=50, *, full_output=True, mode=None, inner=None, k_neighbors=None, device=0,
-         verbose=True, T0=None, method="plane_to_plane", transformation_epsilon=0.0, rotation_epsilon=0.0,
-         euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
+         devices=None, verbose=True, T0=None, method="plane_to_plane", transformation_epsilon=0.0,
+         rotation_epsilon=0.0, euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
     """Drop-in for gicp.py:78 — returns the same 7-tuple (gicp.py:174):
 
     (T, all_transformations, initial_source_cov_matrices, target_cov_matrices,
@@ -471,14 +575,19 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
       inexact inner stop follows the reference's trajectory.
     mode='fast' (3-D default, and larger 2-D clouds): source covariances are
       rotated (rigid invariance), the GPU reduces the loss to its sufficient
-      statistics in one pass, and the inner problem is solved on the host from
-      them -- by fmin_cg on the closed form (inner='cg', 2-D) or exactly by
-      Newton on SO(d) (inner='newton').
+      statistics in one pass, and the inner problem is solved from them -- exactly by
+      Newton on SO(d) (inner='newton', the 3-D default: the whole loop then runs on the
+      device in one gicp_align_trace call, the 7-tuple's per-iteration rows recorded there),
+      or by scipy's fmin_cg on the closed form (inner='cg', the 2-D default, host loop).
     full_output=False skips the per-point visualisation extras (the three
     lists come back empty), which is what large clouds want.  In 'fast' mode the
     top-5 det(W) points are selected on the GPU (no per-point copy) and
     all_source_cov_matrices is a RotatedCovariances view (computed when read).
 
+    device / devices: the GPU, or a list of distinct GPUs; with several, every GPU holds
+      both clouds and reduces its shard of the source, one host thread drives each, and the
+      statistics are summed over them every iteration in device order (the same sum on every
+      GPU, so all take the same step).  mode='faithful' runs on the first listed GPU.
     method: 'plane_to_plane' (GICP, the reference), 'point_to_point' (ICP: C_s = 0,
       C_t = I) or 'point_to_plane' (C_s = 0, C_t = P^-1), presentation/main.typ:446-455.
     transformation_epsilon / rotation_epsilon / euclidean_fitness_epsilon /
@@ -499,7 +608,11 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
         raise ValueError("inner must be 'newton', or 'cg' for 2-D clouds")
     if method not in _lib.COV_MODELS:
         raise ValueError(f"method must be one of {sorted(set(_lib.COV_MODELS))}")
-    eng = _engine(device)
+    devs = _devices(device, devices)
+    if mode == "faithful":
+        devs = devs[:1]
+    engines = [_engine(x) for x in devs]
+    G = len(engines)
     p = default_params(d, max_iterations=int(max_iterations), tolerance=float(tolerance),
                        max_distance_correspondence=float(max_distance_correspondence),
                        max_distance_nearest_neighbors=float(max_distance_nearest_neighbors), k_neighbors=k_neighbors,
@@ -507,21 +620,97 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     pcl = dict(transformation_epsilon=float(transformation_epsilon), rotation_epsilon=float(rotation_epsilon),
                euclidean_fitness_epsilon=float(euclidean_fitness_epsilon),
                mse_relative_epsilon=float(mse_relative_epsilon))
-    use_pcl = any(v > 0 for k, v in pcl.items() if k != "rotation_epsilon")
-    prev_mse = np.inf
-    eng.set_target(tgt, p)
+
+    def build(r, e):
+        e.set_target(tgt, p)
+        e.set_source(src, p, shard=r, nshards=G)
+
+    _run_ranks(engines, build)
+    eng = engines[0]
     target_cov = eng.covariances("target")
-    eng.set_source(src, p)
     init_src_cov = eng.covariances("source")
     T = np.eye(d + 1) if T0 is None else np.array(T0, dtype=np.float64)
+    if mode == "fast" and inner == "newton":
+        for k, v in pcl.items():
+            setattr(p, k, v)
+        return _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, target_cov)
+    return _host_loop(engines, src, tgt, T, T0, p, pcl, mode, inner, full_output, verbose, init_src_cov, target_cov)
+
+
+def _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, target_cov):
+    """gicp.py:116-172 as ONE gicp_align_trace call per GPU: the loop, the solve and the convergence
+    test run on the device; the per-iteration rows the 7-tuple needs (poses, top-5 det(W)) are recorded
+    there and copied out once."""
+    d = src.shape[1]
+    G = len(engines)
+    k = 5 if full_output else 0
+    xchg = _ThreadSum(G) if G > 1 else None
+    if xchg is not None:
+        for r, e in enumerate(engines):
+            e.set_allreduce(lambda buf, r=r: xchg(r, buf))
+
+    def run(r, e):
+        try:
+            return e.align(T, p, trace=True, top_k=k)
+        except BaseException:
+            if xchg is not None:
+                xchg.abort()
+            raise
+
+    try:
+        outs = _run_ranks(engines, run)
+    finally:
+        if xchg is not None:
+            for e in engines:
+                e.set_allreduce(None)
+    T_fin, res, tr = outs[0]
+    iters = int(res["iterations"])
+    poses = tr["poses"]
+    loss_stop = bool(res["converged"]) and res["stop_reason"] == "loss"
+    if res["converged"] and verbose:
+        if loss_stop:
+            print("Converged at iteration", res["converged_at"])                 # gicp.py:161
+        else:
+            print("Converged at iteration", res["converged_at"], f"({res['stop_reason']})")
+    all_T = [T] + [poses[i].copy() for i in range(1, iters)]
+    if iters > 0 and not loss_stop:                                            # gicp.py:166-167
+        all_T.append(T_fin)
+    hw_s, hw_t = [], []
+    all_src_cov = []
+    if full_output:
+        all_src_cov = RotatedCovariances(init_src_cov, [poses[i][:d, :d] for i in range(iters)])   # gicp.py:121
+        for i in range(iters - 1 if loss_stop else iters):                      # gicp.py:169-172
+            rows = [(o[2]["top_src"][i], o[2]["top_tgt"][i], o[2]["top_det"][i]) for o in outs]
+            top_s, top_t, _ = _merge_top(rows) if G > 1 else rows[0]
+            hw_s.append(apply_transformation(src[top_s[top_s >= 0]], poses[i]))
+            hw_t.append(_targets(tgt, top_s, top_t, d))
+    return T_fin, all_T, init_src_cov, target_cov, hw_s, hw_t, all_src_cov
+
+
+def _targets(tgt, top_s, top_t, d):
+    """corresponding_target_points rows of the selected points (gicp.py:140; zeros where rejected)."""
+    ok = top_s >= 0
+    qt = np.zeros((int(ok.sum()), d))
+    m = top_t[ok] >= 0
+    qt[m] = tgt[top_t[ok][m]]
+    return qt
+
+
+def _host_loop(engines, src, tgt, T, T0, p, pcl, mode, inner, full_output, verbose, init_src_cov, target_cov):
+    """gicp.py:116-172 with the inner solve on the host: faithful mode, and fast mode with inner='cg'."""
+    d = src.shape[1]
+    G = len(engines)
+    eng = engines[0]
+    use_pcl = any(v > 0 for k, v in pcl.items() if k != "rotation_epsilon")
+    prev_mse = np.inf
     all_T = [T]
     offset = np.array([T[0, 2], T[1, 2], np.arctan2(T[1, 0], T[0, 0])]) if d == 2 else None
     last = np.inf
     hw_s, hw_t = [], []
-    all_src_cov = [] if (mode == "faithful" or not full_output) else RotatedCovariances(eng, init_src_cov)
+    all_src_cov = [] if (mode == "faithful" or not full_output) else RotatedCovariances(init_src_cov)
     eye = np.eye(d + 1)
     moved_source = False   # faithful mode: the engine holds a transformed copy of the source
-    for it in range(int(max_iterations)):
+    for it in range(int(p.max_iterations)):
         if mode == "faithful":
             moved = apply_transformation(src, T)                   # gicp.py:119
             if it > 0 or T0 is not None:
@@ -541,18 +730,22 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
                 T_new, min_loss = _newton_from_points(src, q, dbg["weight"], idx, T)
                 new_offset = None
         else:
-            if full_output:
-                st, top_s, top_t, _ = eng.iterate_top(T, 5)     # gicp.py:170 on the device
+            if full_output:                                        # gicp.py:170 on the device
+                outs = _run_ranks(engines, lambda r, e: e.iterate_top(T, 5))
+                top_s, top_t, _ = _merge_top([o[1:] for o in outs]) if G > 1 else outs[0][1:]
                 all_src_cov.append_rotation(T[:d, :d])            # gicp.py:120-121, read lazily
             else:
-                st = eng.iterate(T)
+                outs = [(o,) for o in _run_ranks(engines, lambda r, e: e.iterate(T))]
+            st = outs[0][0].copy()
+            for o in outs[1:]:                                     # rank order: deterministic
+                st += o[0]
             if inner == "cg":
                 new_offset, min_loss = _cg_inner(st, offset, T)
                 T_new = _offset_to_T(new_offset)
             else:
                 T_new, min_loss = solve_pose(st, T)
                 new_offset = None
-        if abs(last - min_loss) < tolerance:                       # gicp.py:155-162
+        if abs(last - min_loss) < p.tolerance:                     # gicp.py:155-162
             if verbose:
                 print("Converged at iteration", it)
             break
@@ -566,18 +759,14 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
                 hw_s.append(moved[top])
                 hw_t.append(q[top])
             else:
-                ok = top_s >= 0
-                qt = np.zeros((int(ok.sum()), d))
-                m = top_t[ok] >= 0
-                qt[m] = tgt[top_t[ok][m]]
-                hw_s.append(apply_transformation(src[top_s[ok]], T))   # gicp.py:119,171: the 5 rows only
-                hw_t.append(qt)
+                hw_s.append(apply_transformation(src[top_s[top_s >= 0]], T))   # gicp.py:119,171: the 5 rows only
+                hw_t.append(_targets(tgt, top_s, top_t, d))
         offset = new_offset
         stop = None
         if use_pcl:                                                # PCL-style criteria, after the update
-            info = eng.pass_info()
+            sum_sq = sum(e.pass_info()["sum_sq"] for e in engines)
             cnt = float(np.sum(dbg["index"] >= 0)) if mode == "faithful" else float(st[-1])
-            mse = info["sum_sq"] / cnt if cnt > 0 else 0.0
+            mse = sum_sq / cnt if cnt > 0 else 0.0
             stop = pcl_stop(T, T_new, mse, prev_mse, **pcl)
             prev_mse = mse
         T = T_new

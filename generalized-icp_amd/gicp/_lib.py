@@ -86,6 +86,19 @@ class Debug(C.Structure):
     ]
 
 
+class Trace(C.Structure):
+    """gicp_trace (include/gicp_hip.h): per-iteration rows of gicp_align_trace."""
+    _fields_ = [
+        ("capacity", C.c_int32),
+        ("top_k", C.c_int32),
+        ("poses", C.POINTER(C.c_double)),
+        ("losses", C.POINTER(C.c_double)),
+        ("top_src", C.POINTER(C.c_int64)),
+        ("top_tgt", C.POINTER(C.c_int64)),
+        ("top_det", C.POINTER(C.c_double)),
+    ]
+
+
 # every entry point include/gicp_hip.h declares: name -> (restype, argtypes)
 _VP = C.c_void_p
 _DP = C.POINTER(C.c_double)
@@ -110,6 +123,7 @@ SIGNATURES = {
     "gicp_pass_info": (C.c_int, [_VP, _DP]),
     "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
+    "gicp_align_trace": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result), C.POINTER(Trace)]),
     "gicp_reset_cache": (C.c_int, [_VP]),
     "gicp_stage_target": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params)]),
     "gicp_commit_target": (C.c_int, [_VP, C.c_int, C.c_int]),

@@ -211,6 +211,25 @@ int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_o
  * (k_corr), the statistics exchange when sharded, the pose solve + convergence test (k_solve). */
 int gicp_align(gicp_ctx* ctx, const double* T0, const gicp_params* p, double* T_out, gicp_result* res);
 
+/* What the drop-in's 7-tuple needs from each iteration of that loop (gicp.py:108,121,154,167-172),
+ * recorded on the device while it runs and copied out once at the end.  Caller-allocated; row k is
+ * iteration k (rows >= gicp_result.iterations are untouched).  Any array may be NULL. */
+typedef struct gicp_trace {
+    int32_t capacity;   /* rows the arrays hold: >= gicp_params.max_iterations */
+    int32_t top_k;      /* 0: no top-k rows; 1..16: the pass's k largest det(W) (gicp_top_weights order) */
+    double* poses;      /* [capacity][(dim+1)^2] the pose iteration k's pass ran at (T_k, row-major) */
+    double* losses;     /* [capacity] min_loss of iteration k's inner solve (gicp.py:154) */
+    int64_t* top_src;   /* [capacity][top_k] original source indices (-1 pads) */
+    int64_t* top_tgt;   /* [capacity][top_k] their matched target indices (-1: rejected) */
+    double* top_det;    /* [capacity][top_k] det(W) */
+} gicp_trace;
+/* gicp_align plus the trace (trace = NULL is gicp_align).  With top_k the pass also records det(W)
+ * on the device and two small launches per iteration select the rows (gicp.py:170-172); with a
+ * shard (nshards > 1) the rows cover this rank's shard only -- merge them across ranks by
+ * (det, source index). */
+int gicp_align_trace(gicp_ctx* ctx, const double* T0, const gicp_params* p, double* T_out, gicp_result* res,
+                     gicp_trace* trace);
+
 /* Drop every pose-dependent cache of the current clouds (candidate lists, nearest-neighbour
  * certificates, last matches, seed tiles): the next pass starts cold, as after a fresh
  * gicp_set_source.  Results never depend on the caches (they are exact); only the time does. */

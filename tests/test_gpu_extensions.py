@@ -230,8 +230,8 @@ def test_rotated_covariances_vs_host_einsum(eng, scene3d, dim):
 
 def test_gicp_full_output_rotated_covariances_lazy(scene3d):
     """all_source_cov_matrices of the fast path (gicp.py:121) is a lazy view: one element per executed
-    iteration, each == R_k C_s R_k^T of that iteration's pose (host einsum, 1e-12), on the device while
-    the engine holds the source and from the initial covariances after it changed."""
+    iteration, each == R_k C_s R_k^T of that iteration's pose (host einsum, 1e-12), computed from the
+    initial covariances on the host whatever the engine holds."""
     src, tgt, _ = scene3d
     kw = dict(max_iterations=4, tolerance=0.0, **P3)
     T, all_T, init_cov, _, _, _, all_cov = gicp.gicp(src, tgt, verbose=False, **kw)
