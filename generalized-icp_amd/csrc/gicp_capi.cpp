@@ -1203,18 +1203,16 @@ int gicp_get_covariances(gicp_ctx* c, int which, double* out) {
     return guard_impl(c, "gicp_get_covariances", [&] {
         Cloud& cl = which == 0 ? c->tgt : c->src;
         if (!cl.n || !cl.cov_ready) throw Fail{GICP_E_STATE, "cloud not set"};
+        // a I - m m^T expanded on the device in original order (k_rotate_cov with R = I: R m = m
+        // exactly), then one copy of the n x d x d result
         const int d = cl.dim;
-        std::vector<double4> cv(cl.n);
-        std::vector<int32_t> perm(cl.n);
-        HIPCHK(hipMemcpyAsync(cv.data(), cl.cov, sizeof(double4) * cl.n, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(perm.data(), cl.perm, sizeof(int32_t) * cl.n, hipMemcpyDeviceToHost, c->stream));
+        const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double I2[4] = {1, 0, 0, 1};
+        const size_t m = (size_t)cl.n * d * d;
+        dreserve(c->d_rot, c->cap_rot, m);
+        HIPCHK(launch_rotate_cov(cl.cov, cl.perm, cl.n, d, d == 3 ? I : I2, c->d_rot, c->stream));
+        HIPCHK(hipMemcpyAsync(out, c->d_rot, sizeof(double) * m, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        for (int64_t i = 0; i < cl.n; ++i) {
-            const double m[3] = {cv[i].y, cv[i].z, cv[i].w};
-            double* o = out + (int64_t)perm[i] * d * d;
-            for (int a = 0; a < d; ++a)
-                for (int b = 0; b < d; ++b) o[a * d + b] = (a == b ? cv[i].x : 0.0) - m[a] * m[b];
-        }
     });
 }
 

@@ -2621,8 +2621,8 @@ __global__ void __launch_bounds__(256) k_rotate_cov(const double4* __restrict__ 
 #pragma unroll
     for (int a = 0; a < D; ++a)
 #pragma unroll
-        for (int b = 0; b < D; ++b) o[a * D + b] = (a == b ? c.x : 0.0) - rm[a] * rm[b];
-}
+        for (int b = 0; b < D; ++b) o[a * D + b] = (a == b ? c.x : 0.0) - __dmul_rn(rm[a], rm[b]);   // no fma: the
+}                                                                                                 // host formula's rounding
 
 // ---------------------------------------------------------------------------
 // host-side launchers
