@@ -1,5 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r03d
-timeout -k 10 300 python scripts/probes/full_output_profile.py > gpurun_out/r03d/prof.txt 2> gpurun_out/r03d/prof.err || { tail gpurun_out/r03d/prof.err; exit 1; }
-timeout -k 10 900 python -u -m pytest tests/test_gpu_fullsize.py tests/test_odometry.py -x -v --timeout 600 --timeout-method thread -k "2d or full_size_stream" > gpurun_out/r03d/pytest.log 2>&1; rc=$?; tail -12 gpurun_out/r03d/pytest.log; exit $rc
+OUT=gpurun_out/r03g
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc = 0 ] || { grep -E "FAIL|Error" $OUT/pytest_gpu.log | head; exit 1; }
+bash scripts/bench_variants.sh r03g/ab 3 "GICP_LIB_VARIANT=base" "GICP_LIB_VARIANT=lazy" "GICP_LIB_VARIANT=touch" "X=0" > $OUT/ab.txt 2>&1 || { tail $OUT/ab.txt; exit 1; }
+cat $OUT/ab.txt
+BENCH_ARGS="--shard-sim 8" bash scripts/bench_variants.sh r03g/ab8 2 "GICP_LIB_VARIANT=base" "X=0" > $OUT/ab8.txt 2>&1 || { tail $OUT/ab8.txt; exit 1; }
+cat $OUT/ab8.txt
