@@ -33,10 +33,10 @@ hipError_t launch_morton(const double*, int64_t, int, const DevCloud&, uint32_t*
 hipError_t launch_build_tiles(const double*, int, int32_t*, TileInfo*, int, double*, float4*, int32_t*,
                               unsigned*, hipStream_t);
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
-hipError_t launch_knn_cov(const CovArgs&, int, int, hipStream_t);
+hipError_t launch_knn_cov(const CovArgs&, int, int, bool, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t, double*);
-hipError_t launch_graph(const GraphArgs&, int, hipStream_t);
+hipError_t launch_graph_pack(const GraphArgs&, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
@@ -242,8 +242,6 @@ struct BuildScratch {
     double* h_pinned = nullptr;       // pinned host copy of the input (staged builds)
     size_t cap_pinned = 0;
     std::unique_ptr<WorkerPool> pool;  // tiling threads (lazily started)
-    hipStream_t side = nullptr;       // graph build, concurrent with the covariances
-    hipEvent_t ev = nullptr;
     WorkerPool& workers() {
         if (!pool) {
             const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
@@ -263,10 +261,6 @@ struct BuildScratch {
         if (h_pinned) (void)hipHostFree(h_pinned);
         h_pinned = nullptr;
         pool.reset();
-        if (side) (void)hipStreamDestroy(side);
-        if (ev) (void)hipEventDestroy(ev);
-        side = nullptr;
-        ev = nullptr;
         cap_in = cap_codes = cap_codes2 = cap_idx = cap_sort = cap_gnb = cap_gnbh = cap_pinned = 0;
     }
 };
@@ -656,46 +650,43 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         ca.cov_out = cl.cov;
         ca.count_out = cl.ncount;
         ca.amb_counter = bs.d_amb;
-        // the target neighbour graph (k_corr's graph descent) walks the same cloud as the
-        // covariances but writes other arrays: it runs concurrently on a side stream (each kernel alone
-        // fills only part of the GPU at stream-frame sizes)
-        hipStream_t side = nullptr;
+        // waves per query tile: split small clouds by sub-tile (the walk of one wave bounds them), keep
+        // one wave per tile when the tiles alone fill the GPU (GICP_BUILD_SPLIT = 1 / 4 forces either)
+        static const int split_env = [] {
+            const char* e = std::getenv("GICP_BUILD_SPLIT");
+            return e ? std::atoi(e) : 0;
+        }();
+        ca.split = split_env == 1 || split_env == kSub ? split_env : (cl.ntiles <= 8192 ? kSub : 1);
+        // the target neighbour graph (k_corr's graph descent) comes out of the covariances'
+        // own two walks (k_knn_cov<D, K, true>), then one pass packs the rows
+        GraphArgs ga{};
         if (graph) {
-            if (!bs.side) {
-                HIPCHK(hipStreamCreateWithFlags(&bs.side, hipStreamNonBlocking));
-                HIPCHK(hipEventCreateWithFlags(&bs.ev, hipEventDisableTiming));
-            }
-            side = bs.side;
             dreserve(cl.nbq, cl.cap_nbq, (size_t)n * 8);
             dreserve(cl.nbi, cl.cap_nbi, (size_t)n * kGraphK);
             dreserve(bs.g_nb, bs.cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
             dreserve(bs.g_nbh, bs.cap_gnbh, (size_t)n);
-            GraphArgs ga{};
             ga.cl = cl.view();
+            ga.split = ca.split;
             ga.mg = ca.mg;
             ga.search2 = ca.search2;
             ga.nb = bs.g_nb;
             ga.nbh = bs.g_nbh;
             ga.nbq = cl.nbq;
             ga.nbi = cl.nbi;
-            HIPCHK(hipEventRecord(bs.ev, st));
-            HIPCHK(hipStreamWaitEvent(side, bs.ev, 0));
-            HIPCHK(launch_graph(ga, dim, side));
+            ca.g_nb = bs.g_nb;
+            ca.g_nbh = bs.g_nbh;
         }
         HIPCHK(hipMemsetAsync(cl.ncount, 0, sizeof(int32_t) * n, st));
-        hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, st);
+        hipError_t e = launch_knn_cov(ca, dim, p.k_neighbors, graph, st);
         if (e == hipErrorInvalidValue) throw Fail{GICP_E_INVALID, "unsupported k_neighbors for this dim (2-D: 6, 10; 3-D: 10, 20)"};
         HIPCHK(e);
+        if (graph) HIPCHK(launch_graph_pack(ga, st));
         HIPCHK(hipStreamSynchronize(st));
         cl.cov_ready = true;
         cl.cov_q_begin = qb;
         cl.cov_q_end = qe;
-        tick("covariances");
-        if (side) {
-            HIPCHK(hipStreamSynchronize(side));
-            cl.graph_ready = true;
-            tick("graph");
-        }
+        cl.graph_ready = graph;
+        tick(graph ? "covariances+graph" : "covariances");
         if (verbose)
             std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f | ms:%s\n",
                          (long long)n, cl.ntiles, cl.ntiles / std::ceil(n / 64.0), cl.level, cl.rho, tlog.c_str());

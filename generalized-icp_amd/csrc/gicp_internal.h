@@ -93,6 +93,7 @@ struct Margin {
 
 struct GraphArgs {
     DevCloud cl;
+    int32_t split;            // waves per query tile (1, or kSub: one wave per 16-row sub-tile), see CovArgs
     float search2;            // fp32 screen bound (d_n^2 + margins): the graph's neighbourhood cap
     Margin mg;
     float4* nb;               // [n][kGraphK] scratch: x_t - x_i fp32, t as the w bits
@@ -105,6 +106,10 @@ static_assert(8 + 6 * kGraphK <= 128, "a graph row is one 128-B line");
 struct CovArgs {
     DevCloud cl;
     int32_t q_begin, q_end;   // query tiles
+    // waves per query tile: 1 (the tile's 64 points, one per lane), or kSub (one wave per 16-row sub-tile,
+    // its box the sub-box: a small cloud -- a 100k stream frame is ~1.7k tiles, a third of one wave per
+    // SIMD -- is bound by its longest neighbourhood walk, which the smaller box shortens)
+    int32_t split;
     float search2;            // fp32 screen bound (d_n^2 + margins)
     double dn2;               // d_n^2, fp64, strict
     Margin mg;
@@ -114,6 +119,8 @@ struct CovArgs {
     double4* cov_out;         // [n] sorted
     int32_t* count_out;       // [n] sorted
     int32_t* amb_counter;     // diagnostics (may be null)
+    float4* g_nb;             // k_knn_cov<D, K, true>: the graph rows (GraphArgs::nb), [n][kGraphK]
+    float2* g_nbh;            // ... and (r, count) per point (GraphArgs::nbh)
 };
 
 // Device-resident state of the outer loop (gicp.py:106-110,155-167): the pose every pass reads,

@@ -841,19 +841,21 @@ __device__ __forceinline__ double4 cov_descriptor(const CovSums<D>& A, int min_n
     return out;
 }
 
-template <int D, int K>
-__global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
-    __shared__ WaveLds s_lds[kWavesPerWG];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int T = A.q_begin + blockIdx.x * kWavesPerWG + w;
-    if (T >= A.q_end) return;  // waves are independent (no workgroup barrier here)
-    WaveLds& L = s_lds[w];
-    const DevCloud& cl = A.cl;
-    const TileInfo qt = tile_meta(cl, T);
-
-    Query<D> q;
-    q.valid = l < qt.count;
-    const int i = qt.start + min(l, qt.count - 1);
+// The wave's query for split build kernels: wave `wid` takes part g = wid % split of query tile
+// T = first + wid / split.  Lanes keep their points relative to the tile centre (the screen's error model
+// is unchanged); the culling box `qb` is the part's sub-box (centre c + sc, half-extents sh) when split.
+// Returns the tile index, -1 if the wave has no rows.
+template <int D>
+__device__ __forceinline__ int split_query(const DevCloud& cl, int first, int last, int split, TileInfo& qt,
+                                          Query<D>& q, Query<D>& qb, int& i) {
+    const int wid = (int)blockIdx.x * kWavesPerWG + ((int)threadIdx.x >> 6), l = (int)threadIdx.x & 63;
+    const int T = first + wid / split, g = wid % split;
+    if (T >= last) return -1;
+    qt = tile_meta(cl, T);
+    const int rows = kTile / split, r0 = g * rows, r1 = min(qt.count, r0 + rows);
+    if (r0 >= r1) return -1;
+    q.valid = l < r1 - r0;
+    i = qt.start + r0 + min(l, r1 - r0 - 1);
     const float4 rel = cl.rel32[i];
     const double4 p4 = reinterpret_cast<const double4*>(cl.xyz64)[i];
     const float relv[3] = {rel.x, rel.y, rel.z};
@@ -865,15 +867,43 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         q.pw[a] = relv[a];
         q.p64[a] = p4v[a];
     }
+    qb = q;
+    if (split > 1) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            qb.ow[a] = qt.c[a] + (double)qt.sc[a][g];
+            qb.ew[a] = qt.sh[a][g] * (1.0f + 4.8e-7f) + 1e-30f;
+        }
+    }
+    return T;
+}
+
+// G: the target's neighbour graph rows come out of the same two walks: phase 1 keeps the
+// KL = max(K + 1, kGraphK + 2) smallest keys (the covariance uses the first K + 1, the graph all), phase 2
+// visits every tile either needs and takes each row for the covariance sums (key <= tau) and / or the
+// graph row (key <= tau_g).  Tiles are visited in the same order whatever the bound, so the sums and rows
+// are those of separate walks, bit for bit.
+template <int D, int K, bool G>
+__global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
+    __shared__ WaveLds s_lds[kWavesPerWG];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    WaveLds& L = s_lds[w];
+    const DevCloud& cl = A.cl;
+    TileInfo qt;
+    Query<D> q, qb;
+    int i = 0;
+    const int T = split_query<D>(cl, A.q_begin, A.q_end, A.split, qt, q, qb, i);
+    if (T < 0) return;  // waves are independent (no workgroup barrier here)
 
     // ---- phase 1: fp32 screen for the K+1 smallest keys ------------------
-    constexpr int K1 = K + 1;
+    constexpr int K1 = K + 1, KG = kGraphK, KL = G ? (K1 > KG + 2 ? K1 : KG + 2) : K1;
     const unsigned init = __float_as_uint(A.search2) | 63u;
-    unsigned lk[K1];
+    unsigned lk[KL];
 #pragma unroll
-    for (int m = 0; m < K1; ++m) lk[m] = init;
+    for (int m = 0; m < KL; ++m) lk[m] = init;
     auto lane_bound = [&]() -> float {
         if (!q.valid) return -1.f;
+        if (G) return key_d2(lk[KL - 1]);   // >= the covariance's own bound below
         const float kk = key_d2(lk[K1 - 1]), km = key_d2(lk[K1 - 2]);
         return fminf(kk, km + 2.f * marg(A.mg, km));
     };
@@ -882,18 +912,36 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
         float pr[D];
         const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
         if (!__any(need)) return false;
+        // sub-tiles beyond the top of the truncation bucket of each lane's last list key hold no row the
+        // list would take (a key below it screens at most at that bucket's top)
+        const unsigned sub = sub_mask<D>(ti, pr, q.valid, __uint_as_float((lk[KL - 1] | 63u) + 1u));
         stage_f32(cl, ti, L);
         scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
-            if (__any(key < lk[K1 - 1])) {
+            if (__any(key < lk[KL - 1])) {
 #pragma unroll
-                for (int m = K1 - 1; m > 0; --m) lk[m] = umed3(lk[m - 1], lk[m], key);
+                for (int m = KL - 1; m > 0; --m) lk[m] = umed3(lk[m - 1], lk[m], key);
                 lk[0] = min(lk[0], key);
             }
-        });
+        }, sub);
         wave_sync();
         return true;
     };
-    traverse<D>(cl, q, T, visit1, [&]() { return wave_maxf(lane_bound()); });
+    traverse<D>(cl, qb, T, visit1, [&]() { return wave_maxf(lane_bound()); });
+
+    // graph: rows keyed <= tau_g (the (kGraphK + 1)-th key, self excluded from the row) and the radius the
+    // row certifies (k_graph's rules: from the (kGraphK + 2)-th key, or the screen radius)
+    unsigned tau_g = 0;
+    float r2g = 0.f, tau_g_hi = -1.f;
+    if constexpr (G) {
+        tau_g = lk[KG];
+        if (lk[KG + 1] >= init) {
+            r2g = A.search2 - marg(A.mg, A.search2);
+        } else {
+            const float kd = key_d2(lk[KG + 1] > tau_g ? lk[KG + 1] : tau_g);
+            r2g = kd - marg(A.mg, kd);
+        }
+        tau_g_hi = tau_g >= init ? A.search2 : __uint_as_float((tau_g | 63u) + 1u);
+    }
 
     int c = 0;
 #pragma unroll
@@ -923,11 +971,17 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
     const bool take_lane = q.valid && !amb;
     // cull by the top of tau's truncation bucket: a point keyed <= tau may screen above key_d2(tau)
     const float tau_hi = __uint_as_float((tau | 63u) + 1u);
+    // the lane's phase-2 bound: the covariance's, and the graph row's
+    const float b2 = fmaxf(take_lane ? tau_hi : -1.f, (G && q.valid) ? tau_g_hi : -1.f);
+    int gcnt = 0;
+    bool gover = false;
+    float4* row_out = G ? A.g_nb + (int64_t)i * KG : nullptr;
     auto visit2 = [&](int Tt) -> bool {
         const TileInfo ti = tile_meta(cl, Tt);
         float pr[D];
-        const bool need = take_lane && lane_gap2<D>(q, ti, pr) <= tau_hi;
+        const bool need = lane_gap2<D>(q, ti, pr) <= b2;
         if (!__any(need)) return false;
+        const unsigned sub = sub_mask<D>(ti, pr, b2 >= 0.f, b2);
         stage_f32(cl, ti, L);
         stage_f64(cl, ti, L);
         scan_tile<D>(L, ti.count, pr, [&](unsigned key, int j) {
@@ -939,11 +993,31 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
                 for (int a = 0; a < D; ++a) d[a] = qq[a] - q.p64[a];
                 if (take) cov_add<D>(S, d);
             }
-        });
+            if constexpr (G) {
+                const int t = ti.start + j;
+                if (q.valid && key <= tau_g && t != i) {
+                    if (gcnt < KG) {
+                        const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
+                        float v[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int a = 0; a < D; ++a) v[a] = (float)(qq[a] - q.p64[a]);
+                        row_out[gcnt] = make_float4(v[0], v[1], v[2], __int_as_float(t));
+                        ++gcnt;
+                    } else {
+                        gover = true;
+                    }
+                }
+            }
+        }, sub);
         wave_sync();
         return true;
     };
-    traverse<D>(cl, q, T, visit2, [&]() { return wave_maxf(take_lane ? tau_hi : -1.f); });
+    traverse<D>(cl, qb, T, visit2, [&]() { return wave_maxf(b2); });
+    if (G && q.valid) {
+        // r rounded down; an overflowing row (ties at tau beyond kGraphK) certifies nothing
+        const float r = gover ? 0.f : __builtin_amdgcn_sqrtf(fmaxf(r2g, 0.f)) * 0.99999f;
+        A.g_nbh[i] = make_float2(r, __int_as_float(gcnt));
+    }
 
     // ---- fp64 fallback for lanes the screen could not decide ----------------
     if (__any(amb)) {
@@ -973,7 +1047,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
             wave_sync();
             return true;
         };
-        traverse<D>(cl, q, T, visit3, [&]() { return wave_maxf(amb ? bound_f : -1.f); });
+        traverse<D>(cl, qb, T, visit3, [&]() { return wave_maxf(amb ? bound_f : -1.f); });
         int c64 = 0;
 #pragma unroll
         for (int m = 0; m < K; ++m) c64 += lk64[m] < A.dn2 ? 1 : 0;
@@ -1007,7 +1081,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
             wave_sync();
             return true;
         };
-        traverse<D>(cl, q, T, visit4, [&]() {
+        traverse<D>(cl, qb, T, visit4, [&]() {
             const float b64 = (float)tau64;
             return wave_maxf(amb ? b64 + 2.f * marg(A.mg, b64) : -1.f);
         });
@@ -1020,109 +1094,15 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// target neighbour graph: for every target point i its kGraphK nearest other
-// target points (relative positions + sorted indices) and a radius r(i) such that EVERY target
-// t != i with true |x_t - x_i| < r(i) is in the row.  Built once per target cloud; k_corr's graph
-// descent proves nearest neighbours with it.  Only conservativeness of r matters (no tie rules):
-//   phase 1 keeps the K1 = kGraphK + 2 smallest screened keys (self included);
-//   phase 2 emits the rows keyed <= tau = the (kGraphK + 1)-th key, self excluded;
-//   a row not emitted has a screened key > tau, so its true d2 >= key_d2(lk[K1 - 1]) - margin when
-//   that key is above tau (else key_d2(tau) - margin); a lane that found fewer keys than K1 within
-//   the screen radius has every target within it: r2 = search2 - margin.
-// ---------------------------------------------------------------------------
-template <int D>
-__global__ void __launch_bounds__(256) k_graph(GraphArgs A) {
-    constexpr int KG = kGraphK, K1 = KG + 2;
-    __shared__ WaveLds s_lds[kWavesPerWG];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int T = blockIdx.x * kWavesPerWG + w;
-    if (T >= A.cl.ntiles) return;
-    WaveLds& L = s_lds[w];
-    const DevCloud& cl = A.cl;
-    const TileInfo qt = tile_meta(cl, T);
-    Query<D> q;
-    q.valid = l < qt.count;
-    const int i = qt.start + min(l, qt.count - 1);
-    const float4 rel = cl.rel32[i];
-    const double4 p4 = reinterpret_cast<const double4*>(cl.xyz64)[i];
-    const float relv[3] = {rel.x, rel.y, rel.z};
-    const double p4v[3] = {p4.x, p4.y, p4.z};
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-        q.ow[a] = qt.c[a];
-        q.ew[a] = qt.h[a];
-        q.pw[a] = relv[a];
-        q.p64[a] = p4v[a];
-    }
-    const unsigned init = __float_as_uint(A.search2) | 63u;
-    unsigned lk[K1];
-#pragma unroll
-    for (int m = 0; m < K1; ++m) lk[m] = init;
-    auto lane_bound = [&]() -> float { return q.valid ? key_d2(lk[K1 - 1]) : -1.f; };
-    auto visit1 = [&](int Tt) -> bool {
-        const TileInfo ti = tile_meta(cl, Tt);
-        float pr[D];
-        const bool need = lane_gap2<D>(q, ti, pr) <= lane_bound();
-        if (!__any(need)) return false;
-        stage_f32(cl, ti, L);
-        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int) {
-            if (__any(key < lk[K1 - 1])) {
-#pragma unroll
-                for (int m = K1 - 1; m > 0; --m) lk[m] = umed3(lk[m - 1], lk[m], key);
-                lk[0] = min(lk[0], key);
-            }
-        });
-        wave_sync();
-        return true;
-    };
-    traverse<D>(cl, q, T, visit1, [&]() { return wave_maxf(lane_bound()); });
-
-    const unsigned tau = lk[KG];
-    float r2;
-    if (lk[K1 - 1] >= init) {   // fewer than K1 targets inside the screen radius: all of them are rows
-        r2 = A.search2 - marg(A.mg, A.search2);
-    } else {
-        const float kd = key_d2(lk[K1 - 1] > tau ? lk[K1 - 1] : tau);
-        r2 = kd - marg(A.mg, kd);
-    }
-    const float tau_hi = tau >= init ? A.search2 : __uint_as_float((tau | 63u) + 1u);
-    int cnt = 0;
-    bool over = false;
-    float4* row_out = A.nb + (int64_t)i * KG;
-    auto visit2 = [&](int Tt) -> bool {
-        const TileInfo ti = tile_meta(cl, Tt);
-        float pr[D];
-        const bool need = q.valid && lane_gap2<D>(q, ti, pr) <= tau_hi;
-        if (!__any(need)) return false;
-        stage_f32(cl, ti, L);
-        stage_f64(cl, ti, L);
-        scan_tile<D>(L, ti.count, pr, [&](unsigned key, int j) {
-            const int t = ti.start + j;
-            const bool take = q.valid && key <= tau && t != i;
-            if (take) {
-                if (cnt < KG) {
-                    const double qq[3] = {L.t.x64[j], L.t.y64[j], L.t.z64[j]};
-                    float v[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int a = 0; a < D; ++a) v[a] = (float)(qq[a] - q.p64[a]);
-                    row_out[cnt] = make_float4(v[0], v[1], v[2], __int_as_float(t));
-                    ++cnt;
-                } else {
-                    over = true;
-                }
-            }
-        });
-        wave_sync();
-        return true;
-    };
-    traverse<D>(cl, q, T, visit2, [&]() { return wave_maxf(q.valid ? tau_hi : -1.f); });
-    if (q.valid) {
-        // r rounded down; an overflowing row (ties at tau beyond kGraphK) certifies nothing
-        const float r = over ? 0.f : __builtin_amdgcn_sqrtf(fmaxf(r2, 0.f)) * 0.99999f;
-        A.nbh[i] = make_float2(r, __int_as_float(cnt));
-    }
-}
-
+// target neighbour graph: for every target point i its kGraphK nearest other target
+// points (relative positions + sorted indices) and a radius r(i) such that EVERY target t != i with true
+// |x_t - x_i| < r(i) is in the row.  Built once per target cloud by k_knn_cov<D, K, true> (the same walks
+// as the covariances); k_corr's graph descent proves nearest neighbours with it.  Only conservativeness of
+// r matters (no tie rules): phase 1 keeps the kGraphK + 2 smallest screened keys (self included); phase 2
+// emits the rows keyed <= tau = the (kGraphK + 1)-th key, self excluded; a row not emitted has a screened
+// key > tau, so its true d2 >= key_d2(lk[kGraphK + 1]) - margin when that key is above tau (else
+// key_d2(tau) - margin); a lane that found fewer keys within the screen radius has every target within it:
+// r2 = search2 - margin.
 // Pack the graph rows into one 128-B line each (GraphArgs / DevCloud::nbq): offsets quantised to
 // int16 in units of s = max |offset| / 32767 (error <= s / 2 per axis, which k_corr's bound adds).
 __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ nb, const float2* __restrict__ nbh,
@@ -2665,23 +2645,27 @@ hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blo
     return hipGetLastError();
 }
 
-hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, hipStream_t st) {
+hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, bool graph, hipStream_t st) {
     const int nq = a.q_end - a.q_begin;
     if (nq <= 0) return hipSuccess;
-    const unsigned g = (unsigned)((nq + kWavesPerWG - 1) / kWavesPerWG);
-    if (dim == 2 && k == 6) hipLaunchKernelGGL((k_knn_cov<2, 6>), dim3(g), dim3(256), 0, st, a);
-    else if (dim == 3 && k == 20) hipLaunchKernelGGL((k_knn_cov<3, 20>), dim3(g), dim3(256), 0, st, a);
-    else if (dim == 3 && k == 10) hipLaunchKernelGGL((k_knn_cov<3, 10>), dim3(g), dim3(256), 0, st, a);
-    else if (dim == 2 && k == 10) hipLaunchKernelGGL((k_knn_cov<2, 10>), dim3(g), dim3(256), 0, st, a);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
+    if (a.split != 1 && a.split != kSub) return hipErrorInvalidValue;
+    const unsigned g = (unsigned)(((int64_t)nq * a.split + kWavesPerWG - 1) / kWavesPerWG);
+#define GICP_KNN(DD, KK)                                                                              \
+    if (dim == DD && k == KK) {                                                                        \
+        if (graph) hipLaunchKernelGGL((k_knn_cov<DD, KK, true>), dim3(g), dim3(256), 0, st, a);        \
+        else hipLaunchKernelGGL((k_knn_cov<DD, KK, false>), dim3(g), dim3(256), 0, st, a);             \
+        return hipGetLastError();                                                                      \
+    }
+    GICP_KNN(2, 6)
+    GICP_KNN(3, 20)
+    GICP_KNN(3, 10)
+    GICP_KNN(2, 10)
+#undef GICP_KNN
+    return hipErrorInvalidValue;
 }
 
-hipError_t launch_graph(const GraphArgs& a, int dim, hipStream_t st) {
-    if (a.cl.ntiles <= 0) return hipSuccess;
-    const unsigned g = (unsigned)((a.cl.ntiles + kWavesPerWG - 1) / kWavesPerWG);
-    if (dim == 2) hipLaunchKernelGGL(k_graph<2>, dim3(g), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_graph<3>, dim3(g), dim3(256), 0, st, a);
+hipError_t launch_graph_pack(const GraphArgs& a, hipStream_t st) {
+    if (a.cl.n <= 0) return hipSuccess;
     const unsigned gp = (unsigned)((a.cl.n + 255) / 256);
     hipLaunchKernelGGL(k_graph_pack, dim3(gp), dim3(256), 0, st, a.nb, a.nbh, a.cl.n, a.nbq, a.nbi);
     return hipGetLastError();
