@@ -317,16 +317,20 @@ struct gicp_ctx {
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
     BuildScratch bs;
-    // staged target (gicp_stage_target / gicp_commit_target): built into `next` on stream2 by a host
-    // thread while the current target is registered
-    Cloud next;
-    BuildScratch bs2;
-    hipStream_t stream2 = nullptr;
-    std::thread stager;
-    bool staged = false;
-    int stage_rc = GICP_OK;
-    std::string stage_err;
-    gicp_params pnext{};
+    // staged targets (gicp_stage_target / gicp_commit_target): a ring of GICP_MAX_STAGED slots, each
+    // built into its own cloud on its own stream by a host thread while the current target is
+    // registered; commits take them in staging order
+    struct Staged {
+        Cloud cl;
+        BuildScratch bs;
+        hipStream_t stream = nullptr;
+        std::thread th;
+        gicp_params p{};
+        int rc = GICP_OK;
+        std::string err;
+    };
+    Staged stg[GICP_MAX_STAGED];
+    int stg_head = 0, stg_count = 0;
     size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0;
     int pass = 0;
     bool use_lists = true;
@@ -1058,7 +1062,8 @@ int gicp_create(gicp_ctx** out, int device) {
 
 void gicp_destroy(gicp_ctx* c) {
     if (!c) return;
-    if (c->stager.joinable()) c->stager.join();   // a staged build still running
+    for (auto& g : c->stg)
+        if (g.th.joinable()) g.th.join();        // staged builds still running
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -1086,9 +1091,11 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_list_rcert);
     dfree(c->d_poses);
     c->bs.release();
-    c->bs2.release();
-    c->next.release();
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (auto& g : c->stg) {
+        g.bs.release();
+        g.cl.release();
+        if (g.stream) (void)hipStreamDestroy(g.stream);
+    }
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->h_top) (void)hipHostFree(c->h_top);
     if (c->h_xchg) (void)hipHostFree(c->h_xchg);
@@ -1462,62 +1469,67 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
 int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_stage_target", [&] {
-        if (c->staged) throw Fail{GICP_E_STATE, "a staged target is pending (gicp_commit_target or gicp_cancel_stage first)"};
+        if (c->stg_count >= GICP_MAX_STAGED)
+            throw Fail{GICP_E_STATE, "GICP_MAX_STAGED staged targets are pending (gicp_commit_target or gicp_cancel_stage first)"};
         if (!xyz || M <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
-        c->pnext = resolve(dim, p);
-        if (!c->stream2) HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+        gicp_ctx::Staged& g = c->stg[(c->stg_head + c->stg_count) % GICP_MAX_STAGED];
+        g.p = resolve(dim, p);
+        if (!g.stream) HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
         const size_t need = (size_t)M * dim;
-        if (need > c->bs2.cap_pinned) {   // grow-only pinned staging buffer (allocated here, not in the worker)
-            if (c->bs2.h_pinned) HIPCHK(hipHostFree(c->bs2.h_pinned));
-            c->bs2.h_pinned = nullptr;
-            c->bs2.cap_pinned = 0;
+        if (need > g.bs.cap_pinned) {   // grow-only pinned staging buffer (allocated here, not in the worker)
+            if (g.bs.h_pinned) HIPCHK(hipHostFree(g.bs.h_pinned));
+            g.bs.h_pinned = nullptr;
+            g.bs.cap_pinned = 0;
             const size_t cap = need + need / 8;
-            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->bs2.h_pinned), sizeof(double) * cap));
-            c->bs2.cap_pinned = cap;
+            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&g.bs.h_pinned), sizeof(double) * cap));
+            g.bs.cap_pinned = cap;
         }
-        c->staged = true;
-        c->stage_rc = GICP_OK;
-        c->stage_err.clear();
+        g.rc = GICP_OK;
+        g.err.clear();
         const bool graph = c->use_graph && c->use_certs;
         const int dev = c->device;
-        c->stager = std::thread([c, xyz, M, dim, graph, dev] {
+        gicp_ctx::Staged* gp = &g;
+        g.th = std::thread([gp, xyz, M, dim, graph, dev] {
             try {
                 HIPCHK(hipSetDevice(dev));
-                std::memcpy(c->bs2.h_pinned, xyz, sizeof(double) * (size_t)M * dim);
-                build_cloud(c->next, c->bs2.h_pinned, M, dim, c->pnext, graph, c->bs2, c->stream2, true);
+                std::memcpy(gp->bs.h_pinned, xyz, sizeof(double) * (size_t)M * dim);
+                build_cloud(gp->cl, gp->bs.h_pinned, M, dim, gp->p, graph, gp->bs, gp->stream, true);
             } catch (const Fail& f) {
-                c->stage_rc = f.code;
-                c->stage_err = f.msg;
+                gp->rc = f.code;
+                gp->err = f.msg;
             } catch (const std::bad_alloc&) {
-                c->stage_rc = GICP_E_NOMEM;
-                c->stage_err = "out of host memory";
+                gp->rc = GICP_E_NOMEM;
+                gp->err = "out of host memory";
             } catch (...) {
-                c->stage_rc = GICP_E_INVALID;
-                c->stage_err = "unknown error";
+                gp->rc = GICP_E_INVALID;
+                gp->err = "unknown error";
             }
         });
+        ++c->stg_count;
     });
 }
 
 int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_commit_target", [&] {
-        if (!c->staged) throw Fail{GICP_E_STATE, "no staged target (gicp_stage_target first)"};
-        if (c->stager.joinable()) c->stager.join();
-        c->staged = false;
-        if (c->stage_rc != GICP_OK) throw Fail{c->stage_rc, "staged build: " + c->stage_err};
+        if (!c->stg_count) throw Fail{GICP_E_STATE, "no staged target (gicp_stage_target first)"};
+        gicp_ctx::Staged& g = c->stg[c->stg_head];
+        if (g.th.joinable()) g.th.join();
+        c->stg_head = (c->stg_head + 1) % GICP_MAX_STAGED;
+        --c->stg_count;
+        if (g.rc != GICP_OK) throw Fail{g.rc, "staged build: " + g.err};
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         // the current target (index + covariances) becomes the source, as robot-visualization.py:250
-        // swaps scans, and the staged cloud the target; the old source's buffers wait in `next`
+        // swaps scans, and the staged cloud the target; the old source's buffers wait in the slot
         if (c->tgt.n) {
             std::swap(c->src, c->tgt);
             c->psrc = c->ptgt;
         }
-        std::swap(c->tgt, c->next);
-        c->next.n = 0;
-        c->next.cov_ready = false;
-        c->next.graph_ready = false;
-        c->ptgt = c->pnext;
+        std::swap(c->tgt, g.cl);
+        g.cl.n = 0;
+        g.cl.cov_ready = false;
+        g.cl.graph_ready = false;
+        c->ptgt = g.p;
         c->top_ready = false;
         if (c->src.n) set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -1526,8 +1538,9 @@ int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
 
 int gicp_cancel_stage(gicp_ctx* c) {
     if (!c) return GICP_E_INVALID;
-    if (c->stager.joinable()) c->stager.join();
-    c->staged = false;
+    for (auto& g : c->stg)
+        if (g.th.joinable()) g.th.join();
+    c->stg_head = c->stg_count = 0;
     return GICP_OK;
 }
 

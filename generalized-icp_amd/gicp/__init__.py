@@ -113,7 +113,7 @@ class Engine:
         self.dim = None
         self.n_src = self.n_tgt = 0
         self.generation = 0        # bumped whenever the source cloud changes (lazy covariance views)
-        self._staged = None        # (array, params) of a staged target: kept alive until committed
+        self._staged = []          # (array, params) of the staged targets, oldest first: kept alive until committed
         self._hook = None          # keeps the ctypes callback of set_allreduce alive
 
     def close(self):
@@ -171,27 +171,32 @@ class Engine:
         self.n_tgt = 0
         self.generation += 1
 
+    MAX_STAGED = 2   # GICP_MAX_STAGED
+
     def stage_target(self, pts, params=None):
-        """Build `pts` as the NEXT target on a second stream while the current one is registered
-        (gicp_stage_target); gicp_commit_target (commit_target) makes it current."""
+        """Build `pts` as a coming target on its own stream while the current one is registered
+        (gicp_stage_target; up to MAX_STAGED pending); commit_target makes the oldest current.  The
+        library reads `pts` on its build thread: do not modify the array until that commit returns."""
         a = self._cloud(pts)
         p = params or default_params(a.shape[1])
         check(self._lib.gicp_stage_target(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p)), self._ctx,
               "gicp_stage_target")
-        self._staged = (a, p)
+        self._staged.append((a, p))
 
     def commit_target(self, shard=0, nshards=1):
-        """Wait for the staged target; the current target becomes the source, the staged one the target."""
-        staged, self._staged = self._staged, None
-        check(self._lib.gicp_commit_target(self._ctx, shard, nshards), self._ctx, "gicp_commit_target")
+        """Wait for the oldest staged target; the current target becomes the source, the staged one the target."""
+        rc = self._lib.gicp_commit_target(self._ctx, shard, nshards)
+        staged = self._staged.pop(0) if (self._staged and rc != _lib.GICP_E_STATE) else None   # slot consumed
+        check(rc, self._ctx, "gicp_commit_target")
         if self.n_tgt:
             self.n_src = self.n_tgt
             self.generation += 1
         self.n_tgt, self.dim = staged[0].shape
 
     def cancel_stage(self):
+        """Wait for and drop every staged target."""
         self._lib.gicp_cancel_stage(self._ctx)
-        self._staged = None
+        self._staged = []
 
     def covariances(self, which="target"):
         w = 0 if which == "target" else 1

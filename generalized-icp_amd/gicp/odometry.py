@@ -3,11 +3,12 @@
 
 Each new scan becomes the target; the previous target, with its index and covariances already on
 the GPU, becomes the source (`gicp_target_to_source`, robot-visualization.py:250) — so per frame
-only the new scan is uploaded, sorted, tiled and given covariances.  Given the next scan
-(`step(scan, next_scan)` / `run(scans)`), that build runs on a second stream from a host thread
-while the current pair is registered (`gicp_stage_target` / `gicp_commit_target`), so setup leaves
-the critical path (the demo likewise prepares the next scan while its worker registers,
-robot-visualization.py:239-252).  `gicp(prev, cur)` maps the
+only the new scan is uploaded, sorted, tiled and given covariances.  Given the coming scans
+(`step(scan, next_scan)` / `run(scans, depth)`), their builds run on their own streams from host
+threads while the current pair is registered (`gicp_stage_target` / `gicp_commit_target`, up to
+GICP_MAX_STAGED ahead), so setup leaves the critical path (the demo likewise prepares the next scan
+while its worker registers, robot-visualization.py:239-252).  A staged scan is read by the library's
+build thread: the caller must not modify a scan array until the step that registers it returns.  `gicp(prev, cur)` maps the
 previous sensor frame into the current one (p_cur = T p_prev), so the sensor pose advances by
 T^-1: `composition='se3'` (default) is that exact SE(d) update; `composition='reference'` is the
 demo's first-order update (robot-visualization.py:257-265: translation -T[:2, d], yaw
@@ -42,31 +43,41 @@ class Odometry:
         self.yaw_xy = (0.0, 0.0, 0.0)        # reference-formula state (x, y, yaw)
         self.last_T = None
         self.frames = 0
-        if getattr(self, "_staged", None) is not None:
+        if getattr(self, "_staged", None):
             self.eng.cancel_stage()
-        self._staged = None                  # the scan object whose build is staged
+        self._staged = []                    # the scan objects whose builds are staged, oldest first
         self.timing = {"setup_s": 0.0, "align_s": 0.0, "iterations": 0}
 
     def _prep(self, scan):
         return np.ascontiguousarray(np.asarray(scan, dtype=np.float64)[:, :self.dim])
 
-    def step(self, scan, next_scan=None):
+    def step(self, scan, next_scan=None, next_scans=()):
         """Add one scan; returns (T, result) of its registration against the previous scan, or
-        (None, None) for the first frame.  `next_scan`, if given, is built on the device while this
-        pair is registered; pass the same object as `scan` of the next call."""
+        (None, None) for the first frame.  `next_scan` (or the list `next_scans`, at most
+        Engine.MAX_STAGED), if given, is built on the device while this pair is registered; pass the
+        same objects as `scan` of the next calls, in order.  Scans must not be modified until the
+        step that registers them returns (the library reads them on its build threads)."""
         t0 = time.perf_counter()
-        if self._staged is not None and self._staged is scan:
-            self.eng.commit_target()            # built during the last registration
+        if self._staged and self._staged[0] is scan:
+            self.eng.commit_target()            # built during an earlier registration
+            self._staged.pop(0)
         else:
-            if self._staged is not None:
+            if self._staged:
                 self.eng.cancel_stage()
+                self._staged = []
             if self.frames > 0:
                 self.eng.target_to_source()
             self.eng.set_target(self._prep(scan), self.params)
-        self._staged = None
-        if next_scan is not None:
-            self.eng.stage_target(self._prep(next_scan), self.params)
-            self._staged = next_scan
+        coming = list(next_scans) if next_scan is None else [next_scan, *next_scans]
+        for k, s in enumerate(coming[:self.eng.MAX_STAGED]):
+            if k < len(self._staged):
+                if self._staged[k] is not s:    # a different stream than staged: start over
+                    self.eng.cancel_stage()
+                    self._staged = []
+                else:
+                    continue
+            self.eng.stage_target(self._prep(s), self.params)
+            self._staged.append(s)
         t1 = time.perf_counter()
         self.timing["setup_s"] += t1 - t0
         self.frames += 1
@@ -80,15 +91,23 @@ class Odometry:
         self._integrate(T)
         return T, res
 
-    def run(self, scans):
-        """Register a whole stream (each scan's build overlapped with the previous registration);
-        yields (T, result) per scan."""
+    def run(self, scans, depth=2):
+        """Register a whole stream, each scan's build started `depth` registrations ahead (1: during the
+        previous registration; 2, the default: during the two before it, so a build that takes longer
+        than one registration stays off the critical path); yields (T, result) per scan."""
+        depth = max(1, min(int(depth), self.eng.MAX_STAGED))
         it = iter(scans)
-        cur = next(it, None)
-        while cur is not None:
+        window = []
+        for s in it:
+            window.append(s)
+            if len(window) > depth:
+                break
+        while window:
+            cur = window.pop(0)
             nxt = next(it, None)
-            yield self.step(cur, nxt)
-            cur = nxt
+            if nxt is not None:
+                window.append(nxt)
+            yield self.step(cur, next_scans=window[:depth])
 
     def _integrate(self, T):
         self.pose, self.yaw_xy = compose(self.pose, T, self.composition, self.yaw_xy)

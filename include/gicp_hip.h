@@ -43,7 +43,8 @@ extern "C" {
 #define GICP_E_NOMEM (-5)     /* host or device allocation failed */
 
 #define GICP_COMM_ID_BYTES 128
-#define GICP_MAX_STATS 74     /* statistics per pass, dim 3 (dim 2: 26) */
+#define GICP_MAX_STATS 74     /* statistics per pass, dim 3 (dim 2: 26); a multi-GPU exchange carries these
+                                 plus the GICP_PASS_INFO diagnostics: 80 fp64 (dim 2: 32) */
 
 typedef struct gicp_ctx gicp_ctx;
 
@@ -153,12 +154,14 @@ int gicp_set_source(gicp_ctx* ctx, const double* xyz, int64_t N, int dim, const 
  * as robot-visualization.py:250 swaps scans; then set a new target. */
 int gicp_target_to_source(gicp_ctx* ctx, int shard, int nshards);
 
-/* Double-buffered frame stream (robot-visualization.py:239-252): build the
- * NEXT target -- pinned copy, upload, Morton sort, tiling, covariances, neighbour graph -- on a
- * second stream from a host thread while the current target is registered (gicp_align on the
- * first stream runs concurrently).  `xyz` must stay valid until gicp_commit_target returns.
- * gicp_commit_target waits for the build, then promotes: current target -> source (as
- * gicp_target_to_source), staged cloud -> target.  gicp_cancel_stage waits and drops it. */
+/* Pipelined frame stream (robot-visualization.py:239-252): build the NEXT
+ * targets -- pinned copy, upload, Morton sort, tiling, covariances, neighbour graph -- each on its own
+ * stream from a host thread while the current target is registered (gicp_align on the library's stream
+ * runs concurrently).  Up to GICP_MAX_STAGED builds may be pending; commits take them in staging
+ * order.  `xyz` must stay valid, and unmodified, until the gicp_commit_target that takes it returns.
+ * gicp_commit_target waits for the oldest build, then promotes: current target -> source (as
+ * gicp_target_to_source), staged cloud -> target.  gicp_cancel_stage waits for and drops them all. */
+#define GICP_MAX_STAGED 2
 int gicp_stage_target(gicp_ctx* ctx, const double* xyz, int64_t M, int dim, const gicp_params* p);
 int gicp_commit_target(gicp_ctx* ctx, int shard, int nshards);
 int gicp_cancel_stage(gicp_ctx* ctx);

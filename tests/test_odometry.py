@@ -77,14 +77,19 @@ def test_staged_stream_equals_synchronous_stream():
     kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
     frames = [f for f, _ in S.lidar_stream(6, beams=32, azimuths=900)]
     out = {}
-    for mode in ("sync", "staged"):
+    for mode in ("sync", "staged1", "staged2"):
         odo = Odometry(3, params=gicp.default_params(3, max_iterations=30, tolerance=1e-9, **kw))
-        Ts = [odo.step(f)[0] for f in frames] if mode == "sync" else [T for T, _ in odo.run(frames)]
+        if mode == "sync":
+            Ts = [odo.step(f)[0] for f in frames]
+        else:   # builds started one or two registrations ahead (GICP_MAX_STAGED pending)
+            Ts = [T for T, _ in odo.run(frames, depth=int(mode[-1]))]
         out[mode] = (Ts, odo.pose.copy())
         odo.eng.close()
-    for a, b in zip(out["sync"][0][1:], out["staged"][0][1:]):
-        assert np.array_equal(a, b)
-    assert np.array_equal(out["sync"][1], out["staged"][1])
+    for mode in ("staged1", "staged2"):
+        assert len(out[mode][0]) == len(frames)
+        for a, b in zip(out["sync"][0][1:], out[mode][0][1:]):
+            assert np.array_equal(a, b)
+        assert np.array_equal(out["sync"][1], out[mode][1])
 
 
 @pytest.mark.gpu
@@ -139,3 +144,36 @@ def test_full_size_stream_per_frame_vs_oracle():
         checked += 1
     odo.eng.close()
     assert checked == 10
+
+
+@pytest.mark.gpu
+def test_stage_ring_limits_and_order():
+    """gicp_stage_target keeps up to GICP_MAX_STAGED builds pending and commits them in staging order;
+    one more is refused (GICP_E_STATE), a commit with none pending too, cancel drops them all."""
+    import gicp
+    from gicp import _lib
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    f = [s for s, _ in S.lidar_stream(5, beams=16, azimuths=400)]
+    p = gicp.default_params(3, **kw)
+    eng = gicp.Engine(0)
+    try:
+        eng.set_target(f[0], p)
+        eng.stage_target(f[1], p)
+        eng.stage_target(f[2], p)
+        with pytest.raises(_lib.GicpError):
+            eng.stage_target(f[3], p)
+        eng.commit_target()
+        assert eng.n_tgt == len(f[1]) and eng.n_src == len(f[0])
+        eng.commit_target()
+        assert eng.n_tgt == len(f[2]) and eng.n_src == len(f[1])
+        with pytest.raises(_lib.GicpError):
+            eng.commit_target()
+        eng.stage_target(f[3], p)
+        eng.stage_target(f[4], p)
+        eng.cancel_stage()
+        with pytest.raises(_lib.GicpError):
+            eng.commit_target()
+        T, res = eng.align(None, gicp.default_params(3, max_iterations=5, **kw))
+        assert np.all(np.isfinite(T))
+    finally:
+        eng.close()
