@@ -532,7 +532,7 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
 // Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
 // is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
-                 BuildScratch& bs, hipStream_t st, bool pinned_input = false) {
+                 BuildScratch& bs, hipStream_t st, bool staged = false) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -595,7 +595,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         uint32_t *d_codes = bs.s_codes, *d_codes_s = bs.s_codes2;
         int32_t* d_idx = bs.s_idx;
         // (a staged build passes its pinned copy: the H2D copy is then asynchronous)
-        (void)pinned_input;
         HIPCHK(hipMemcpyAsync(d_in, xyz, sizeof(double) * n * dim, hipMemcpyHostToDevice, st));
         DevCloud fr = cl.view();
         HIPCHK(launch_morton(d_in, n, dim, fr, d_codes, d_idx, st));
@@ -654,13 +653,15 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         ca.cov_out = cl.cov;
         ca.count_out = cl.ncount;
         ca.amb_counter = bs.d_amb;
-        // waves per query tile: split small clouds by sub-tile (the walk of one wave bounds them), keep
-        // one wave per tile when the tiles alone fill the GPU (GICP_BUILD_SPLIT = 1 / 4 forces either)
+        // waves per query tile: a synchronous build of a small cloud is split by sub-tile (the walk of its
+        // longest wave bounds it); a staged build keeps one wave per tile -- it runs beside a registration,
+        // whose k_corr the split's idle lanes would slow (C5, 500 frames: 1050 vs 960 frames/s) -- and so
+        // does a cloud whose tiles alone fill the GPU (GICP_BUILD_SPLIT = 1 / 4 forces either)
         static const int split_env = [] {
             const char* e = std::getenv("GICP_BUILD_SPLIT");
             return e ? std::atoi(e) : 0;
         }();
-        ca.split = split_env == 1 || split_env == kSub ? split_env : (cl.ntiles <= 8192 ? kSub : 1);
+        ca.split = split_env == 1 || split_env == kSub ? split_env : (!staged && cl.ntiles <= 8192 ? kSub : 1);
         // the target neighbour graph (k_corr's graph descent) comes out of the covariances'
         // own two walks (k_knn_cov<D, K, true>), then one pass packs the rows
         GraphArgs ga{};
