@@ -98,7 +98,8 @@ typedef struct gicp_result {
     double final_loss;         /* min_loss of the last inner solve */
     int64_t correspondences;   /* accepted correspondences in the last pass, all ranks */
     double wall_ms;            /* host wall time of the iteration loop */
-    double corr_kernel_ms;     /* correspondence-kernel time: mean HIP-event duration of every 8th launch x iterations */
+    double corr_kernel_ms;     /* correspondence-kernel time: mean HIP-event duration of the sampled launches
+                                  (gicp_params.timing_stride / timing_offset) x iterations executed */
     double reduce_ms;          /* sum of HIP-event durations of partial-reduce + all-reduce */
     int64_t pairs_evaluated;   /* source x target distance evaluations in the last pass (if counted) */
     int32_t stop_reason;       /* GICP_STOP_* */

@@ -1,10 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r03l
+OUT=gpurun_out/r03m
 mkdir -p $OUT
-for r in 1 2; do
-for v in "GICP_BUILD_SPLIT=1" "GICP_BUILD_SPLIT=4"; do
-env $v timeout -k 10 300 python bench_odometry.py --frames 500 > $OUT/odo_${v}_$r.json 2> $OUT/odo.err || { tail $OUT/odo.err; exit 1; }
-python -c "import json;d=json.load(open('$OUT/odo_${v}_$r.json'));print('$v', {k:round(d[k],3) for k in ('value','frames_per_s','setup_ms_per_frame','align_ms_per_frame')})"
-done
-done
+GICP_LIB_VARIANT=stamps timeout -k 10 300 python scripts/pass_diag.py 1000000 12 > $OUT/diag.txt 2> $OUT/stamps.txt || { tail $OUT/stamps.txt; exit 1; }
+tail -14 $OUT/diag.txt
+grep -E "all |slowest|median|mean cycles" $OUT/stamps.txt | head -60 | cut -c1-400
+timeout -k 10 400 python scripts/twod_1m_vs_oracle.py > $OUT/twod_1m.json 2> $OUT/twod.err || { tail $OUT/twod.err; exit 1; }
+cat $OUT/twod_1m.json
