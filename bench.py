@@ -142,8 +142,8 @@ def measured_traffic(workload):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload:
-            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
-    return None, None
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT), d.get("per_pass")
+    return None, None, None
 
 
 def cpu_baseline(src, tgt, kw, workers, iters=1):
@@ -284,7 +284,7 @@ def main():
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
     n_mov = min(10, a.steps)
     pairs = res["pairs_total"] / a.steps / world   # mean per launch (summed over ranks by the all-reduce)
-    traffic, traffic_src = measured_traffic(name) if world == 1 else (None, None)
+    traffic, traffic_src, traffic_pp = measured_traffic(name) if world == 1 else (None, None, None)
     line = {
         "metric": "GICP iterations/sec (and ms/iter) at N points, 1/2/4/8 GPU; final transform error",
         "value": a.steps / elapsed,
@@ -307,6 +307,11 @@ def main():
         "comm": comm_kind,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_per_pass": None if not traffic_pp else
+                     {k: traffic_pp.get(k) for k in ("first_pass", "moving_mean", "converged_mean", "timed_mean")},
+                     "traffic_vs_alg": None if not traffic_pp else
+                     {k: round(traffic_pp[k] / alg_bytes, 2) for k in ("first_pass", "moving_mean", "converged_mean")
+                      if traffic_pp.get(k)},
                      "kernel": "k_corr", "kernel_avg_ms": corr_avg_ms, "alg_bytes_per_launch": alg_bytes,
                      "alg_bytes_rule": f"SURVEY.md 8(d): {bytes_per_point(a.dim)} B x (N/G + M)",
                      "impl_bytes_per_launch": impl_bytes,

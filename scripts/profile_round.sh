@@ -1,11 +1,11 @@
 #!/bin/bash
 # Round profile of the default bench command: kernel-trace stats, per-iteration trace, PMC passes
-# (instruction mix, waits) and the HBM-side traffic summary; then the bench line (which reads the
-# traffic just measured).  Usage: scripts/profile_round.sh OUTNAME PROFILEDIR   (e.g. r02 profiles/r02)
+# (instruction mix, waits) and the HBM-side traffic summary, mean and per pass; then the bench line (which
+# reads the traffic just measured).  Usage: scripts/profile_round.sh OUTNAME PROFILEDIR   (e.g. r03 profiles/r03)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
-PD=${2:-profiles/r02}
+PD=${2:-profiles/r03}
 mkdir -p $OUT $PD
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o t --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/trace.err || { echo trace failed; exit 1; }
 python3 scripts/trace_iters.py $OUT/trace 30 > $OUT/iterations.txt
