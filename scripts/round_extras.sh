@@ -15,3 +15,5 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 python3 scripts/pmc_passes.py $OUT/pmc/p1 > $OUT/pmc_passes.txt
 for f in bench_c2 bench_2d_1m bench_2d_100k; do python3 -c "import json;d=json.load(open('$OUT/$f.json'));print('$f',round(d['value'],1),d['unit'],'k_corr',round(d['roofline']['kernel_avg_ms']*1e3,1),'us')"; done
 cat $OUT/bench_odometry_staged.json | head -c 600; echo
+timeout -k 10 300 python scripts/full_output_cost.py > $OUT/full_output_cost.json 2> $OUT/foc.err || { echo full_output_cost failed; tail $OUT/foc.err; exit 1; }
+cat $OUT/full_output_cost.json
