@@ -310,6 +310,7 @@ struct gicp_ctx {
     size_t cap_cj = 0, cap_cg = 0, cap_cp = 0;
     bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
     bool use_graph = true;            // GICP_NO_GRAPH=1: no target neighbour graph, no graph descent
+    bool fuse_solve = true;           // GICP_FUSE_SOLVE=0: the solve as its own k_solve launch even with no exchange
     int unit_map = 0;                 // k_corr workgroup -> unit map (CorrArgs::unit_map, GICP_UNIT_MAP)
     int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
@@ -1036,6 +1037,7 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_NO_GRAPH")) c->use_graph = !(e[0] == '1');
+    if (const char* e = std::getenv("GICP_FUSE_SOLVE")) c->fuse_solve = !(e[0] == '0');
     if (const char* e = std::getenv("GICP_UNIT_MAP")) c->unit_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
@@ -1381,6 +1383,13 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                     a.dbg_det = c->d_dbg_det;
                     a.top_tgt = c->d_top_tgt;
                 }
+                // no exchange of the statistics between ranks: k_corr's final workgroup runs the solve too
+                const bool fuse = c->fuse_solve && grid > 0 && !c->hook && !c->comm;
+                double* const hist = trace ? c->d_hist + (size_t)it * HS : nullptr;
+                if (fuse) {
+                    a.fuse_solve = 1;
+                    a.hist = hist;
+                }
                 const bool ev = timing && it % kEvStride == kEvOffset;
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b], st));
                 if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
@@ -1391,8 +1400,10 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                                               c->d_top_i, kTopBlocks, c->d_trace_det + (size_t)it * 16,
                                               c->d_trace_top + (size_t)it * 32, c->d_trace_top + (size_t)it * 32 + 16,
                                               st));
-                allreduce_stats(c);
-                HIPCHK(launch_solve(c->d_state, d, st, trace ? c->d_hist + (size_t)it * HS : nullptr));
+                if (!fuse) {
+                    allreduce_stats(c);
+                    HIPCHK(launch_solve(c->d_state, d, st, hist));
+                }
             }
             enq += B;
             HIPCHK(hipMemcpyAsync(&hs, c->d_state, sizeof(IterState), hipMemcpyDeviceToHost, st));

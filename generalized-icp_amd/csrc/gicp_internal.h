@@ -206,6 +206,10 @@ struct CorrArgs {
     float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
     float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected
     unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
+    // 1: the final workgroup also runs the inner solve + pose update (what k_solve does), when no exchange
+    // of the statistics between ranks comes between them; `hist` = this iteration's gicp_trace row or null
+    int32_t fuse_solve;
+    double* hist;
 };
 
 constexpr int nstat(int D) {

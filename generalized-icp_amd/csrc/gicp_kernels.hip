@@ -24,6 +24,7 @@
 
 #include "gicp_internal.h"
 #include "gicp_solver.h"
+#include "gicp_solve_dev.h"
 
 namespace gicp {
 
@@ -125,11 +126,6 @@ struct Stamps {
     __device__ __forceinline__ void count(int, unsigned = 1) {}
 #endif
 };
-
-// Diagnostic hook of the solve's stages (a probe build defines it; nothing otherwise)
-#ifndef GICP_SOLVE_STAMP
-#define GICP_SOLVE_STAMP(k) ((void)0)
-#endif
 
 // exact-rounding fp64 square distance, summed in axis order without FMA contraction
 // (the order a KD-tree accumulates it in)
@@ -1194,13 +1190,6 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
     return 1.0;
 }
 
-// LDS the one-wave solve exchanges through
-template <int D>
-struct SolveLds {
-    static constexpr int NR = D * D, M = D == 2 ? 1 : 3;
-    double kc[D][NR], u[NR], hd[M][NR], f[2][NR];   // f double-buffered: one barrier per loss evaluation
-};
-
 template <int D>
 __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
@@ -2110,313 +2099,24 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     }
     __syncthreads();
     if (!s_last) return;
+    // the final workgroup.  With no exchange between ranks it also runs the solve and the pose update
+    // (gicp_solve_dev.h, one wave) -- the state header is requested now, in flight with the reduction's loads
+    const bool fuse = A.fuse_solve != 0;
+    double hv = 0.0;
+    if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     sum_rows(A.gpart, 0, ng, s_sum);
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// solve_pose_t (gicp_solver.h) restated for one wave: the reduced NR x NR Hessian H' is built and
-// held one row per lane (lane i < NR), so the matrix-vector products of the damped Newton loop
-// (H' dr, H' D_l, the loss) are lane-parallel and meet through LDS; the small dense work
-// (the M x M Newton system, the rotation update) runs redundantly in every lane, which keeps
-// the control flow uniform. Same iterates as the serial solver up to summation order.
-template <int D, class Sync>
-__device__ __forceinline__ SolveOut<D> solve_pose_wave(const double* st, const double* Tk, SolveLds<D>& sl, Sync sync) {
-    using namespace solver_detail;
-    constexpr int NS = D * (D + 1) / 2, NR = D * D, N1 = D + 1, M = D == 2 ? 1 : 3;
-    auto& s_kc = sl.kc;
-    auto& s_u = sl.u;
-    auto& s_hd = sl.hd;
-    auto& s_f = sl.f;
-    const int lane = threadIdx.x;
-    const int i = lane < NR ? lane : 0;   // lanes >= NR shadow row 0 and never store
-    SolveOut<D> out;
-    out.ok = 1;
-#pragma unroll
-    for (int k = 0; k < N1 * N1; ++k) out.T[k] = Tk[k];
-    out.loss = 0.0;
-    const double* A = st;
-    const double* B = A + NS * NS;
-    const double* C = B + NS * D;
-    const double* gR = C + NS;
-    const double* gt = gR + D * D;
-    const double c0 = gt[D];
-    if (!(gt[D + 1] > 0.5)) return out;
-
-    double Rk[NR], tk[D];
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-#pragma unroll
-        for (int b = 0; b < D; ++b) Rk[a * D + b] = Tk[a * N1 + b];
-        tk[a] = Tk[a * N1 + D];
-    }
-    double Ht[D][D], Hti[D][D];
-#pragma unroll
-    for (int a = 0; a < D; ++a)
-#pragma unroll
-        for (int b = 0; b < D; ++b) Ht[a][b] = C[sym<D>(a, b)];
-    if (!spd_inv<D>(Ht, Hti)) {
-        out.ok = 0;
-        return out;
-    }
-    double kt[D];
-    {
-        double rhs[D], x[D];
-#pragma unroll
-        for (int a = 0; a < D; ++a) rhs[a] = gt[a];
-        sym_mul<D>(Hti, rhs, kt);
-        // column i of K = Htt^-1 Htr on lane i
-        const int ci = i / D, cj = i % D;
-#pragma unroll
-        for (int b = 0; b < D; ++b) rhs[b] = B[sym<D>(ci, b) * D + cj];
-        sym_mul<D>(Hti, rhs, x);
-        if (lane < NR)
-#pragma unroll
-            for (int a = 0; a < D; ++a) s_kc[a][lane] = x[a];
-    }
-    sync();
-    // row i of H' and g'_i
-    double Hrow[NR], gpi;
-    {
-        const int ia = i / D, ii = i % D;
-        double bi[D];
-#pragma unroll
-        for (int a = 0; a < D; ++a) bi[a] = B[sym<D>(ia, a) * D + ii];
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            double s = A[sym<D>(ia, j / D) * NS + sym<D>(ii, j % D)];
-#pragma unroll
-            for (int a = 0; a < D; ++a) s -= bi[a] * s_kc[a][j];
-            Hrow[j] = s;
-        }
-        gpi = gR[i];
-#pragma unroll
-        for (int a = 0; a < D; ++a) gpi -= bi[a] * kt[a];
-    }
-    double c0p = c0;
-#pragma unroll
-    for (int a = 0; a < D; ++a) c0p -= gt[a] * kt[a];
-
-    // loss at R (phi of the serial solver) and, on lane i, u_i = (H' dr - g')_i
-    int fbuf = 0;
-    auto eval = [&](const double (&Rv)[NR], double& ui) {
-        double hi = 0.0, dri = 0.0;
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const double dr = Rv[j] - Rk[j];
-            hi += Hrow[j] * dr;
-            dri = j == i ? dr : dri;
-        }
-        ui = hi - gpi;
-        // alternate buffers: a buffer is rewritten two evaluations later, and every path between
-        // passes a barrier after its reads (this eval's or the next iteration's), so no second one here
-        double* const fb = s_f[fbuf];
-        fbuf ^= 1;
-        if (lane < NR) fb[lane] = dri * hi - 2.0 * gpi * dri;
-        sync();
-        double f = c0p;
-#pragma unroll
-        for (int j = 0; j < NR; ++j) f += fb[j];
-        return f;
-    };
-
-    double R[NR];
-#pragma unroll
-    for (int k = 0; k < NR; ++k) R[k] = Rk[k];
-    // at R = R_k: dr = 0, so u_i = -g'_i and the loss is c0' exactly (what eval(R_k) would return)
-    double ui = -gpi;
-    GICP_SOLVE_STAMP(2);
-    double f = c0p;
-    GICP_SOLVE_STAMP(3);
-    double lam = 0.0;
-    for (int it = 0; it < 100; ++it) {
-        GICP_SOLVE_STAMP(4 + min(it, 3));
-        if (lane < NR) {
-            s_u[lane] = ui;
-#pragma unroll
-            for (int l = 0; l < M; ++l) s_hd[l][lane] = gdot<D>(l, R, Hrow);   // (H' vec(G_l R))_i
-        }
-        sync();
-        GICP_SOLVE_STAMP(8);
-        // grad_k = 2 u.vec(G_k R) and the second-order term u.vec(1/2 (G_k G_l + G_l G_k) R) of the
-        // serial solver, through P = R U^T (U = u as a D x D matrix): u.vec(X R) = tr(X P),
-        // G_k G_l = e_l e_k^T - delta_kl I in 3-D and G^2 = -I in 2-D.
-        double P[D][D];
-#pragma unroll
-        for (int a = 0; a < D; ++a)
-#pragma unroll
-            for (int b = 0; b < D; ++b) {
-                double s = 0.0;
-#pragma unroll
-                for (int c = 0; c < D; ++c) s += R[a * D + c] * s_u[b * D + c];
-                P[a][b] = s;
-            }
-        double grad[M], Hs[M][M];
-        if constexpr (D == 2) {
-            grad[0] = 2.0 * (P[0][1] - P[1][0]);
-        } else {
-            grad[0] = 2.0 * (P[1][2] - P[2][1]);
-            grad[1] = 2.0 * (P[2][0] - P[0][2]);
-            grad[2] = 2.0 * (P[0][1] - P[1][0]);
-        }
-        double trP = 0.0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) trP += P[a][a];
-#pragma unroll
-        for (int k = 0; k < M; ++k)
-#pragma unroll
-            for (int l = k; l < M; ++l) {
-                const double s = gdot<D>(k, R, s_hd[l]);
-                const double t2 = D == 2 ? -trP : 0.5 * (P[k][l] + P[l][k]) - (k == l ? trP : 0.0);
-                Hs[k][l] = Hs[l][k] = 2.0 * s + 2.0 * t2;
-            }
-        GICP_SOLVE_STAMP(9);
-        // (no barrier here: s_u / s_hd are rewritten only after the eval below, whose barriers order
-        // these reads; every path to the next iteration runs it)
-        double gmax = 0.0, hscale = 0.0;
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-            gmax = fmax(gmax, fabs(grad[k]));
-            hscale = fmax(hscale, fabs(Hs[k][k]));
-        }
-        if (gmax == 0.0) break;
-        bool stepped = false, flat = false, quad = false;
-        double wmax = 0.0;
-        for (int tries = 0; tries < 60; ++tries) {
-            double Hd[M][M], Hdi[M][M], ng[M], w[M];
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-#pragma unroll
-                for (int l = 0; l < M; ++l) Hd[k][l] = Hs[k][l] + (k == l ? lam * (hscale + 1e-300) : 0.0);
-                ng[k] = -grad[k];
-            }
-            double dd = 0.0;
-            bool ok = spd_inv<M>(Hd, Hdi);
-            if (ok) {
-                sym_mul<M>(Hdi, ng, w);
-#pragma unroll
-                for (int k = 0; k < M; ++k) dd += w[k] * grad[k];
-                ok = dd < 0.0;
-            }
-            GICP_SOLVE_STAMP(10);
-            if (ok) {
-                double Rn[NR], un;
-                rot_update<D>(w, R, Rn);
-                GICP_SOLVE_STAMP(11);
-                const double fn = eval(Rn, un);
-                wmax = 0.0;
-#pragma unroll
-                for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
-                // the model decrease -dd/2 is below the rounding of f: no step can be resolved, stop
-                // instead of damping towards |w| < 1e-15 (the tries would only chase rounding noise)
-                if (fn > f && -dd <= kFlatEps * fabs(f)) {
-                    flat = true;
-                    break;
-                }
-                if (fn <= f || wmax < 1e-15) {
-                    if (fn <= f) {
-#pragma unroll
-                        for (int k = 0; k < NR; ++k) R[k] = Rn[k];
-                        f = fn;
-                        ui = un;
-                    }
-                    stepped = true;
-                    quad = fn <= f && lam == 0.0 && wmax < kQuadStop;   // (f = fn when accepted)
-                    lam = lam > 0.0 ? lam * 0.1 : 0.0;
-                    if (lam < 1e-12) lam = 0.0;
-                    break;
-                }
-            }
-            lam = lam == 0.0 ? 1e-9 : lam * 10.0;
-        }
-        if (!stepped || flat || quad || wmax < 1e-15) break;
-    }
-    GICP_SOLVE_STAMP(12);
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-        double s = kt[a];
-#pragma unroll
-        for (int c = 0; c < NR; ++c) s -= s_kc[a][c] * (R[c] - Rk[c]);
-        out.T[a * N1 + D] = tk[a] + s;
-#pragma unroll
-        for (int b = 0; b < D; ++b) out.T[a * N1 + b] = R[a * D + b];
-    }
-#pragma unroll
-    for (int b = 0; b < D; ++b) out.T[D * N1 + b] = 0.0;
-    out.T[D * N1 + D] = 1.0;
-    out.loss = f;
-    return out;
-}
-
-// The inner solve (gicp.py:148-154) from a pass's statistics, then the convergence test and pose
-// update of gicp.py:155-167, on the device so iterations need no host sync.  Run by one wave (lanes
-// 0-63); `sync` orders that wave's LDS traffic.  `Ls` is an LDS copy of the device state S (header
-// and statistics, loaded in one round trip): everything is read from it, only the results go to S.
-template <int D, class Sync>
-__device__ void solve_update(IterState* S, const IterState* Ls, SolveLds<D>& sl, Sync sync, double* hist) {
-    const int lane = threadIdx.x & 63;
-    constexpr int NSX = nstat_ext(D);
-    const double* st = Ls->stats;
-    if (lane < NSX) S->stats_solved[lane] = st[lane];
-    if (lane + 64 < NSX) S->stats_solved[lane + 64] = st[lane + 64];
-    const SolveOut<D> r = solve_pose_wave<D>(st, Ls->T, sl, sync);
-    if (lane != 0) return;
-    const IterState* SR = Ls;   // the state as this launch found it
-    const int it = SR->iter;
-    if (hist) {   // gicp_trace row of this iteration: the pose its pass ran at, then min_loss
-        constexpr int NT = (D + 1) * (D + 1);
-#pragma unroll
-        for (int k = 0; k < NT; ++k) hist[k] = SR->T[k];
-        hist[NT] = r.loss;
-    }
-    S->iter = it + 1;
-    if (!r.ok) S->solve_fail = 1;
-    S->loss = r.loss;
-    constexpr int NSS = nstat(D);
-    S->pairs_total = SR->pairs_total + st[NSS + 1];
-    const double cnt = st[NSS - 1];
-    const double mse = cnt > 0.0 ? st[NSS + 3] * solver_detail::recip(cnt) : 0.0;
-    S->mse = mse;
-    if (!SR->fixed && fabs(SR->last_loss - r.loss) < SR->tol) {   // gicp.py:160: stop before the update
-        S->converged = 1;
-        S->converged_at = it;
-        S->stop_reason = GICP_STOP_LOSS;
-        return;
-    }
-    S->last_loss = r.loss;
-    // PCL-style criteria on the increment dT = T_new T_old^-1 and the pass's MSE; PCL applies the
-    // update and then tests, so these stop AFTER the update (include/gicp_hip.h GICP_STOP_*)
-    int reason = GICP_STOP_NONE;
-    if (!SR->fixed) {
-        constexpr int N1 = D + 1;
-        double tr = 0.0, tsq = 0.0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) {
-            double dta = r.T[a * N1 + D];
-#pragma unroll
-            for (int b = 0; b < D; ++b) {
-                double dr = 0.0;   // (R_new R_old^T)[a][b]
-#pragma unroll
-                for (int c = 0; c < D; ++c) dr += r.T[a * N1 + c] * SR->T[b * N1 + c];
-                if (a == b) tr += dr;
-                dta -= dr * SR->T[b * N1 + D];
-            }
-            tsq += dta * dta;
-        }
-        const double cosang = D == 3 ? 0.5 * (tr - 1.0) : 0.5 * tr;
-        const double dm = fabs(mse - SR->prev_mse);
-        if (SR->trans_eps > 0.0 && cosang >= SR->rot_cos && tsq <= SR->trans_eps) reason = GICP_STOP_TRANSFORM;
-        else if (SR->fit_eps > 0.0 && dm < SR->fit_eps) reason = GICP_STOP_ABS_MSE;
-        else if (SR->rel_eps > 0.0 && dm / SR->prev_mse < SR->rel_eps) reason = GICP_STOP_REL_MSE;
-        S->prev_mse = mse;
-    }
-#pragma unroll
-    for (int k = 0; k < (D + 1) * (D + 1); ++k) S->T[k] = r.T[k];
-    if (reason != GICP_STOP_NONE) {
-        S->converged = 1;
-        S->converged_at = it;
-        S->stop_reason = reason;
-    }
+    if (!fuse || threadIdx.x >= 64) return;
+    // LDS after the reduction scratch: the header image (its `stats` field unused: the statistics are s_sum)
+    // and the solve's exchange area
+    static_assert(sizeof(double) * 4 * NSX + sizeof(IterState) + sizeof(SolveLds<D>) <= sizeof(WaveLds) * kCorrWaves,
+                  "solve LDS fits the staging LDS");
+    IterState* s_hdr = reinterpret_cast<IterState*>(s_sum + NSX);
+    SolveLds<D>* s_sl = reinterpret_cast<SolveLds<D>*>(s_sum + NSX + sizeof(IterState) / sizeof(double));
+    if (threadIdx.x < kStateHeader) reinterpret_cast<double*>(s_hdr)[threadIdx.x] = hv;
+    wave_sync();
+    solve_update<D>(A.state, s_hdr, s_sum, *s_sl, A.hist);
 }
 
 // One wave: solve_update on the statistics in the device state (after the multi-GPU all-reduce).
@@ -2441,7 +2141,7 @@ __global__ void __launch_bounds__(64) k_solve(IterState* S, double* hist) {
     __syncthreads();
     GICP_SOLVE_STAMP(1);
     if (s_state.converged) return;
-    solve_update<D>(S, &s_state, s_sl, [] { __syncthreads(); }, hist);
+    solve_update<D>(S, &s_state, s_state.stats, s_sl, hist);
     GICP_SOLVE_STAMP(13);
 }
 

@@ -43,6 +43,17 @@ struct SolveOut {
 
 namespace solver_detail {
 
+// A floating-point constant materialised where it is used (device).  fp64 VALU operands cannot be
+// literals on gfx9, so every such constant lives in a register pair, and the compiler hoists them all out
+// of the solve's loops -- ~20 pairs held through the solve, which inside k_corr's 80-VGPR budget spill.
+// The empty volatile asm keeps each one at its use (two s_mov_b32 there).  Identity on the host.
+GICP_HD double kc(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(v));
+#endif
+    return v;
+}
+
 template <int D>
 GICP_HD constexpr int sym(int a, int b) {
     return a <= b ? a * D - a * (a - 1) / 2 + (b - a) : b * D - b * (b - 1) / 2 + (a - b);
@@ -111,39 +122,100 @@ GICP_HD void sym_mul(const double (&Mi)[N][N], const double (&b)[N], double (&x)
     }
 }
 
+// sin and cos of th.  On the device without libm's argument reduction, whose path for huge arguments
+// (Payne-Hanek) needs more registers than the whole one-wave solve may use inside k_corr: th is reduced
+// modulo 2 pi in two parts (Cody-Waite; a huge th only loses accuracy in the angle, never in
+// s^2 + c^2 = 1), halved to below 1/32 (at most 7 times), the series evaluated there (truncation
+// < 3e-18, the same coefficients as rot_update's small-angle branch: every fp64 constant is a register
+// pair in the loop) and the double-angle formulas applied back.  On the host the libm functions.
+GICP_HD void sincos_lean(double th, double& s, double& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double n = rint(th * 0.15915494309189535);             // th / (2 pi)
+    double x = fma(-n, kc(6.28318530717958623e+00), th);        // 2 pi = C1 + C2, C1 = fl(2 pi)
+    x = fma(-n, kc(2.44929359829470641e-16), x);
+    int k = 0;
+    while (!(fabs(x) < 0.03125) && k < 7) {
+        x *= 0.5;
+        ++k;
+    }
+    const double x2 = x * x;
+    s = x * (1.0 + x2 * (kc(-1.0 / 6) + x2 * (kc(1.0 / 120) + x2 * kc(-1.0 / 5040))));
+    c = 1.0 - x2 * (0.5 + x2 * (kc(-1.0 / 24) + x2 * (kc(1.0 / 720) + x2 * kc(-1.0 / 40320))));
+    for (; k > 0; --k) {
+        const double s2 = 2.0 * s * c;
+        c = (c - s) * (c + s);
+        s = s2;
+    }
+#else
+    s = sin(th);
+    c = cos(th);
+#endif
+}
+
+// exp([w]) = c I + s1 [w]x + s2 w w^T (3-D): s1 = sin(th)/th, s2 = (1 - cos th)/th^2, c = cos th = 1 - s2 th^2
+GICP_HD void exp_coeffs(const double* w, double& s1, double& s2, double& c) {
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    if (th2 < kc(9.765625e-4)) {
+        // by their series in th^2 (th < 1/32): truncation < th^8/362880 < 3e-18 here, and neither sin/cos
+        // nor a square root on the device's single-wave solve (the Newton steps are small)
+        s1 = 1.0 + th2 * (kc(-1.0 / 6) + th2 * (kc(1.0 / 120) + th2 * kc(-1.0 / 5040)));
+        s2 = 0.5 + th2 * (kc(-1.0 / 24) + th2 * (kc(1.0 / 720) + th2 * kc(-1.0 / 40320)));
+    } else {
+        const double th = sqrt(th2);
+        double sn, cs;
+        sincos_lean(th, sn, cs);
+        s1 = sn / th;
+        s2 = (1.0 - cs) / th2;
+    }
+    c = 1.0 - s2 * th2;   // ([w]x^2 = w w^T - th^2 I)
+}
+
+// entry (a, b) of exp([w]) R, 3-D, from exp_coeffs
+GICP_HD double exp_mul_entry(const double* w, double s1, double s2, double c, const double* R, int a, int b) {
+    const double wa = a == 0 ? w[0] : a == 1 ? w[1] : w[2];
+    // row a of [w]x: (0, -w2, w1), (w2, 0, -w0), (-w1, w0, 0)
+    const double x0 = a == 0 ? 0.0 : a == 1 ? w[2] : -w[1];
+    const double x1 = a == 0 ? -w[2] : a == 1 ? 0.0 : w[0];
+    const double x2 = a == 0 ? w[1] : a == 1 ? -w[0] : 0.0;
+    const double e0 = (a == 0 ? c : 0.0) + s2 * wa * w[0] + s1 * x0;
+    const double e1 = (a == 1 ? c : 0.0) + s2 * wa * w[1] + s1 * x1;
+    const double e2 = (a == 2 ? c : 0.0) + s2 * wa * w[2] + s1 * x2;
+    return e0 * R[b] + e1 * R[3 + b] + e2 * R[6 + b];
+}
+
 // R <- exp([w]) R (left perturbation)
 template <int D>
 GICP_HD void rot_update(const double* w, const double (&R)[D * D], double (&Rn)[D * D]) {
     if constexpr (D == 2) {
-        const double c = cos(w[0]), s = sin(w[0]);
+        double c, s;
+        sincos_lean(w[0], s, c);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             Rn[b] = c * R[b] - s * R[2 + b];
             Rn[2 + b] = s * R[b] + c * R[2 + b];
         }
     } else {
-        const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-        double s1, s2;
-        if (th2 < 0.0625) {
-            // sin(th)/th and (1-cos th)/th^2 by their series in th^2 (th < 0.25): truncation
-            // < th^12/6e9 < 1e-17 here, and neither libm sin/cos nor a square root on the device's
-            // single-wave solve (the Newton steps are small)
-            s1 = 1.0 + th2 * (-1.0 / 6 + th2 * (1.0 / 120 + th2 * (-1.0 / 5040 + th2 * (1.0 / 362880 + th2 * (-1.0 / 39916800)))));
-            s2 = 0.5 + th2 * (-1.0 / 24 + th2 * (1.0 / 720 + th2 * (-1.0 / 40320 + th2 * (1.0 / 3628800 + th2 * (-1.0 / 479001600)))));
-        } else {
-            const double th = sqrt(th2);
-            s1 = sin(th) / th;
-            s2 = (1.0 - cos(th)) / th2;
-        }
-        // exp([w]) = cos(th) I + s1 [w]x + s2 w w^T  ([w]x^2 = w w^T - th^2 I, cos th = 1 - s2 th^2)
-        const double c = 1.0 - s2 * th2;
-        const double E[9] = {c + s2 * w[0] * w[0], s2 * w[0] * w[1] - s1 * w[2], s2 * w[0] * w[2] + s1 * w[1],
-                             s2 * w[1] * w[0] + s1 * w[2], c + s2 * w[1] * w[1], s2 * w[1] * w[2] - s1 * w[0],
-                             s2 * w[2] * w[0] - s1 * w[1], s2 * w[2] * w[1] + s1 * w[0], c + s2 * w[2] * w[2]};
+        double s1, s2, c;
+        exp_coeffs(w, s1, s2, c);
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int b = 0; b < 3; ++b) Rn[a * 3 + b] = E[a * 3] * R[b] + E[a * 3 + 1] * R[3 + b] + E[a * 3 + 2] * R[6 + b];
+            for (int b = 0; b < 3; ++b) Rn[a * 3 + b] = exp_mul_entry(w, s1, s2, c, R, a, b);
+    }
+}
+
+// entry j of rot_update's result, R in memory (LDS): the device solve computes one entry per lane
+template <int D>
+GICP_HD double rot_update_entry(const double* w, const double* R, int j) {
+    if constexpr (D == 2) {
+        double c, s;
+        sincos_lean(w[0], s, c);
+        const int b = j & 1;
+        return j < 2 ? c * R[b] - s * R[2 + b] : s * R[b] + c * R[2 + b];
+    } else {
+        double s1, s2, c;
+        exp_coeffs(w, s1, s2, c);
+        return exp_mul_entry(w, s1, s2, c, R, j / 3, j % 3);
     }
 }
 

@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < reps; ++r) {
         CK(hipMemcpy(d, H.data(), sizeof(IterState) * P, hipMemcpyHostToDevice));
         CK(hipEventRecord(e0));
-        for (int p = 0; p < P; ++p) hipLaunchKernelGGL(gicp::k_solve<3>, dim3(1), dim3(64), 0, 0, d + p);
+        for (int p = 0; p < P; ++p) hipLaunchKernelGGL(gicp::k_solve<3>, dim3(1), dim3(64), 0, 0, d + p, (double*)nullptr);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -83,7 +83,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_out), &o, sizeof o));
 #endif
         CK(hipMemcpy(d + p, &H[p], sizeof(IterState), hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(gicp::k_solve<3>, dim3(1), dim3(64), 0, 0, d + p);
+        hipLaunchKernelGGL(gicp::k_solve<3>, dim3(1), dim3(64), 0, 0, d + p, (double*)nullptr);
         CK(hipDeviceSynchronize());
     }
     std::vector<unsigned long long> hs(16 * P);
