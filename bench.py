@@ -317,7 +317,10 @@ def main():
                      "impl_bytes_per_launch": impl_bytes,
                      "impl_frac": impl_bytes / (corr_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_timing": "HIP events, every k_corr launch of K timed once (8 identical cold-start "
-                                      "K-iteration runs at sampling offsets 0..7, stride 8)"},
+                                      "K-iteration runs at sampling offsets 0..7, stride 8)",
+                     "kernel_note": ("k_corr's final workgroup also runs the one-wave inner solve and pose update "
+                                     "(~5 us, inside the timed duration)" if world == 1 and a.shard_sim <= 1 else
+                                     "the inner solve is k_solve after the statistics exchange (not in k_corr's time)")},
         "passes": {"moving_pass_us": float(np.mean(per_iter[:n_mov])) * 1e3,
                    "converged_pass_us": float(np.mean(per_iter[-n_mov:])) * 1e3,
                    "first_pass_us": float(per_iter[0]) * 1e3,

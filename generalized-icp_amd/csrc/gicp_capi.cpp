@@ -1383,8 +1383,9 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                     a.dbg_det = c->d_dbg_det;
                     a.top_tgt = c->d_top_tgt;
                 }
-                // no exchange of the statistics between ranks: k_corr's final workgroup runs the solve too
-                const bool fuse = c->fuse_solve && grid > 0 && !c->hook && !c->comm;
+                // one unsharded rank (no exchange of the statistics): k_corr's final workgroup runs the solve too
+                // (a shard without a communicator -- bench.py --shard-sim -- keeps the multi-rank launch shape)
+                const bool fuse = c->fuse_solve && grid > 0 && !c->hook && !c->comm && c->nshards == 1;
                 double* const hist = trace ? c->d_hist + (size_t)it * HS : nullptr;
                 if (fuse) {
                     a.fuse_solve = 1;

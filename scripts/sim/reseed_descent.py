@@ -18,7 +18,7 @@ iters = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 H = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 THRS = [float(x) for x in (sys.argv[4] if len(sys.argv) > 4 else "0.05,0.1,0.2").split(",")]
 LEVELS = [int(x) for x in (sys.argv[5] if len(sys.argv) > 5 else "7,8").split(",")]   # grid bits per axis
-K = 20
+K = int(__import__("os").environ.get("SIM_K", "20"))
 dc, dn = 0.5, 1.0
 src, tgt, Tgt = S.scene_pair_3d(n)
 t0 = time.time()
