@@ -30,7 +30,7 @@
 
 namespace gicp {
 hipError_t launch_morton(const double*, int64_t, int, const DevCloud&, uint32_t*, int32_t*, hipStream_t);
-hipError_t launch_build_tiles(const double*, int, int32_t*, TileInfo*, int, double*, float4*, int32_t*,
+hipError_t launch_build_tiles(const double*, int, int32_t*, TileInfo*, TileBox*, int, double*, float4*, int32_t*,
                               unsigned*, hipStream_t);
 hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipStream_t);
 hipError_t launch_knn_cov(const CovArgs&, int, int, bool, hipStream_t);
@@ -166,6 +166,9 @@ struct Cloud {
     TileInfo* tiles = nullptr;
     BlockInfo* blocks = nullptr;
     uint32_t* tile_code = nullptr;
+    TileBox* boxes = nullptr;         // the walk's compact tile records (k_build_tiles)
+    int32_t* seed_tab = nullptr;      // Morton seed lookup (DevCloud::seed_tab), built on the host
+    int seed_shift = 0;
     uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows
     int32_t* nbi = nullptr;           // ... and their sorted indices
     bool graph_ready = false;
@@ -173,7 +176,7 @@ struct Cloud {
     int cov_q_begin = 0, cov_q_end = 0;  // tiles whose covariances were computed
 
     size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
-    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0;
+    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0, cap_boxes = 0, cap_seed = 0;
     void reserve_points(int64_t np) {
         dreserve(xyz64, cap_xyz, (size_t)np * 4);
         dreserve(rel32, cap_rel, (size_t)np);
@@ -186,6 +189,7 @@ struct Cloud {
         dreserve(tiles, cap_tiles, (size_t)nt);
         dreserve(blocks, cap_blocks, (size_t)nb + (nb + kBlockTiles - 1) / kBlockTiles);   // + super-blocks
         dreserve(tile_code, cap_tcode, (size_t)nt);
+        dreserve(boxes, cap_boxes, (size_t)nt);
     }
     void release() {
         dfree(xyz64);
@@ -197,10 +201,12 @@ struct Cloud {
         dfree(tiles);
         dfree(blocks);
         dfree(tile_code);
+        dfree(boxes);
+        dfree(seed_tab);
         dfree(nbq);
         dfree(nbi);
         cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
-        cap_nbq = cap_nbi = 0;
+        cap_nbq = cap_nbi = cap_boxes = cap_seed = 0;
         n = 0;
         cov_ready = false;
         graph_ready = false;
@@ -214,6 +220,9 @@ struct Cloud {
         v.tiles = tiles;
         v.blocks = blocks;
         v.tile_code = tile_code;
+        v.boxes = boxes;
+        v.seed_tab = seed_tab;
+        v.seed_shift = seed_shift;
         v.nbq = graph_ready ? nbq : nullptr;
         v.nbi = graph_ready ? nbi : nullptr;
         v.n = n;
@@ -630,7 +639,27 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         HIPCHK(hipMemsetAsync(d_rho, 0, sizeof(unsigned), st));
         HIPCHK(hipMemcpyAsync(cl.tiles, ti.data(), sizeof(TileInfo) * cl.ntiles, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(cl.tile_code, tcode.data(), sizeof(uint32_t) * cl.ntiles, hipMemcpyHostToDevice, st));
-        HIPCHK(launch_build_tiles(d_in, dim, cl.perm, cl.tiles, cl.ntiles, cl.xyz64, cl.rel32, cl.inv, d_rho, st));
+        // Morton seed lookup (DevCloud::seed_tab): 2^sb buckets of the code's top bits, about 4 per tile
+        std::vector<int32_t> seed;
+        {
+            const int code_bits = dim * cl.bits;
+            int sb = 2;
+            while ((1 << sb) < 4 * cl.ntiles && sb < 20) ++sb;
+            sb = std::min(sb, code_bits);
+            cl.seed_shift = code_bits - sb;
+            const size_t nb = (size_t)1 << sb;
+            seed.resize(nb + 1);
+            int t = 0;   // last tile whose first code <= p << shift (0 if none)
+            for (size_t p = 0; p < nb; ++p) {
+                const uint64_t lim = (uint64_t)p << cl.seed_shift;
+                while (t + 1 < cl.ntiles && (uint64_t)tcode[t + 1] <= lim) ++t;
+                seed[p] = t;
+            }
+            seed[nb] = cl.ntiles - 1;
+            dreserve(cl.seed_tab, cl.cap_seed, nb + 1);
+            HIPCHK(hipMemcpyAsync(cl.seed_tab, seed.data(), sizeof(int32_t) * (nb + 1), hipMemcpyHostToDevice, st));
+        }
+        HIPCHK(launch_build_tiles(d_in, dim, cl.perm, cl.tiles, cl.boxes, cl.ntiles, cl.xyz64, cl.rel32, cl.inv, d_rho, st));
         HIPCHK(launch_build_blocks(cl.tiles, cl.ntiles, cl.blocks, cl.nblocks, dim, st));
         unsigned rho_bits = 0;
         HIPCHK(hipMemcpyAsync(&rho_bits, d_rho, sizeof(unsigned), hipMemcpyDeviceToHost, st));

@@ -53,6 +53,15 @@ struct __attribute__((aligned(16))) TileInfo {
     float sh[3][kSub];  // sub-tile box half-extents (cover every rel32 of the sub-tile), axis-major
 };
 
+// The walk's view of a tile: what k_corr's candidate tests read for every tile of a candidate block (or
+// list), 48 B so a wave's 64 records are three coalesced 16-B loads per lane (TileInfo is 144 B apart)
+struct __attribute__((aligned(16))) TileBox {
+    double c[3];      // = TileInfo::c
+    float h[3];       // = TileInfo::h
+    uint32_t sc6;     // (start << 6) | (count - 1)   (gicp_set_* keep n < 2^26)
+};
+static_assert(sizeof(TileBox) == 48, "TileBox is three 16-B words");
+
 struct __attribute__((aligned(16))) BlockInfo {
     double c[3];
     float h[3];
@@ -70,6 +79,12 @@ struct DevCloud {
     const TileInfo* tiles;    // [ntiles]
     const BlockInfo* blocks;  // [nblocks] blocks of 64 tiles, then [ceil(nblocks / 64)] super-blocks of 64 blocks
     const uint32_t* tile_code;// [ntiles] Morton code of each tile's first point
+    const TileBox* boxes;     // [ntiles] the walk's compact tile records
+    // Morton seed lookup: seed_tab[p] = the last tile whose first code <= p << seed_shift (0 if none),
+    // p < 2^seed_bits, seed_tab[2^seed_bits] = ntiles - 1: the tile of code c lies in
+    // [seed_tab[c >> seed_shift], seed_tab[(c >> seed_shift) + 1]] (a few binary steps instead of log2 ntiles)
+    const int32_t* seed_tab;
+    int32_t seed_shift;
     // neighbour graph (target only; null when not built), DESIGN.md §3c.  Row i is one 128-B line:
     // dword 0 r(i) (fp32: every target t != i with |x_t - x_i| < r is in the row), dword 1 the scale s,
     // then kGraphK entries of 3 int16 (x_t - x_i) / s, rounded to nearest (|error| <= s / 2 per

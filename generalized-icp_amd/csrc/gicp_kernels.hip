@@ -217,8 +217,8 @@ __device__ __forceinline__ void split_order(double (&p)[3], int& o, int dim, boo
 }
 
 __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ xyz_in, int dim,
-                                                      int32_t* __restrict__ perm, TileInfo* tiles, int ntiles,
-                                                      double* xyz64, float4* rel32, int32_t* inv,
+                                                      int32_t* __restrict__ perm, TileInfo* tiles, TileBox* boxes,
+                                                      int ntiles, double* xyz64, float4* rel32, int32_t* inv,
                                                       unsigned* rho_bits) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int T = blockIdx.x * kWavesPerWG + w;
@@ -284,6 +284,12 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
             t.h[a] = h[a];
         }
         t.radius = rad;
+        TileBox& b = boxes[T];
+        for (int a = 0; a < 3; ++a) {
+            b.c[a] = c[a];
+            b.h[a] = h[a];
+        }
+        b.sc6 = ((uint32_t)start << 6) | (uint32_t)(count - 1);
         atomicMax(rho_bits, __float_as_uint(rad));
     }
 }
@@ -555,54 +561,61 @@ __device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, in
             wbi = infl(wb);
         }
     }
-    typedef __attribute__((address_space(4))) const BlockInfo* ConstBlocks;
-    const ConstBlocks cb0 = (ConstBlocks)(uintptr_t)db.blocks + db.nblocks;
-    for (int b0 = 0; b0 < db.nblocks; b0 += kWave) {
-        {
-            const ConstBlocks sb = cb0 + (b0 / kWave);
-            const double c[3] = {sb->c[0], sb->c[1], sb->c[2]};
-            const float h[3] = {sb->h[0], sb->h[1], sb->h[2]};
-            if (!__builtin_amdgcn_readfirstlane((int)(gap2_box<D>(q, c, h) <= wbi))) continue;   // uniform
-        }
-        if (cnt) cnt->count(5);
-        const int b = b0 + l;
-        bool cb = false;
-        if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wbi;
-        uint64_t bm = __ballot(cb);
-        while (bm) {
-            const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
-            bm &= bm - 1;
-            const int first = db.blocks[bb].first, nt = db.blocks[bb].ntiles;
-            if (cnt) cnt->count(6);
-            const int t = first + l;
-            bool ct = false;
-            float g2 = 3e38f;
-            uint32_t sc6 = 0;   // (start << 6) | (count - 1): one register (gicp_set_* keep n < 2^26)
-            if (l < nt && t != seed) {
-                g2 = gap2_box<D>(q, db.tiles[t].c, db.tiles[t].h);
-                ct = g2 <= wbi;
-                sc6 = ((uint32_t)db.tiles[t].start << 6) | (uint32_t)(db.tiles[t].count - 1);
-            }
-            if (skin > 0.f) {
-                uint64_t cm = __ballot(ct);
-                while (cm) {
-                    collect(first + __ffsll((unsigned long long)cm) - 1);
-                    cm &= cm - 1;
+    // super-blocks (64 blocks each, stored after the blocks): lane s tests super-block s0 + s, all of a
+    // round of 64 requested at once (one memory round trip instead of one per super-block); a candidate
+    // super-block's 64 blocks are tested by the lanes, a candidate block's 64 tiles likewise from the
+    // compact TileBox records (block b's tiles are 64 b .. 64 b + 63).  Same tiles, same order as the
+    // one-super-block-at-a-time walk.
+    const int nsuper = (db.nblocks + kWave - 1) / kWave;
+    for (int s0 = 0; s0 < nsuper; s0 += kWave) {
+        float sg = 3e38f;
+        if (s0 + l < nsuper) sg = gap2_box<D>(q, db.blocks[db.nblocks + s0 + l].c, db.blocks[db.nblocks + s0 + l].h);
+        uint64_t sm = __ballot(sg <= wbi);
+        while (sm) {
+            const int sl = __ffsll((unsigned long long)sm) - 1;
+            sm &= sm - 1;
+            const int b0 = (s0 + sl) * kWave;
+            if (cnt) cnt->count(5);
+            const int b = b0 + l;
+            bool cb = false;
+            if (b < db.nblocks) cb = gap2_box<D>(q, db.blocks[b].c, db.blocks[b].h) <= wbi;
+            uint64_t bm = __ballot(cb);
+            while (bm) {
+                const int bb = b0 + __ffsll((unsigned long long)bm) - 1;
+                bm &= bm - 1;
+                const int first = bb * kBlockTiles, nt = min(kBlockTiles, db.ntiles - first);
+                if (cnt) cnt->count(6);
+                const int t = first + l;
+                bool ct = false;
+                float g2 = 3e38f;
+                uint32_t sc6 = 0;   // (start << 6) | (count - 1)
+                if (l < nt && t != seed) {
+                    const TileBox tb = db.boxes[t];
+                    g2 = gap2_box<D>(q, tb.c, tb.h);
+                    ct = g2 <= wbi;
+                    sc6 = tb.sc6;
                 }
-            }
-            uint64_t tm = __ballot(g2 <= wb);
-            auto pick = [&]() -> int { return tm ? __ffsll((unsigned long long)tm) - 1 : -1; };
-            auto coords = [&](int kk) {
-                const uint32_t v = __builtin_amdgcn_readlane(sc6, kk);
-                return load_rel(db, (int)(v >> 6), (int)(v & 63u) + 1);
-            };
-            for (int k = pick(); k >= 0; k = pick()) {
-                tm &= ~(1ull << k);
-                const float4 pv = coords(k);   // in flight with the tile's metadata load in visit_pre
-                if (visit_pre(first + k, &pv)) {
-                    wb = wave_bound();
-                    wbi = infl(wb);
-                    tm &= __ballot(g2 <= wb);
+                if (skin > 0.f) {
+                    uint64_t cm = __ballot(ct);
+                    while (cm) {
+                        collect(first + __ffsll((unsigned long long)cm) - 1);
+                        cm &= cm - 1;
+                    }
+                }
+                uint64_t tm = __ballot(g2 <= wb);
+                auto pick = [&]() -> int { return tm ? __ffsll((unsigned long long)tm) - 1 : -1; };
+                auto coords = [&](int kk) {
+                    const uint32_t v = __builtin_amdgcn_readlane(sc6, kk);
+                    return load_rel(db, (int)(v >> 6), (int)(v & 63u) + 1);
+                };
+                for (int k = pick(); k >= 0; k = pick()) {
+                    tm &= ~(1ull << k);
+                    const float4 pv = coords(k);   // in flight with the tile's metadata load in visit_pre
+                    if (visit_pre(first + k, &pv)) {
+                        wb = wave_bound();
+                        wbi = infl(wb);
+                        tm &= __ballot(g2 <= wb);
+                    }
                 }
             }
         }
@@ -1288,6 +1301,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (seed < 0 || seed >= tg.ntiles) {
             const uint32_t code = morton_code(q.ow, D, tg.lo, tg.scale, tg.bits);
             int lo = 0, hi = tg.ntiles - 1;
+            if (tg.seed_tab) {   // the bucket's range: both ends in one round trip
+                const uint32_t b = code >> tg.seed_shift;
+                lo = tg.seed_tab[b];
+                hi = tg.seed_tab[b + 1];
+            }
             while (lo < hi) {  // last tile whose first code <= code
                 const int mid = (lo + hi + 1) >> 1;
                 if (tg.tile_code[mid] <= code) lo = mid;
@@ -1657,7 +1675,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         key = 0.f;
 #pragma unroll
                         for (int a = 0; a < D; ++a) {
-                            const float d = (float)(tg.tiles[cent].c[a] - q.ow[a]);
+                            const float d = (float)(tg.boxes[cent].c[a] - q.ow[a]);
                             key = fmaf(d, d, key);
                         }
                     }
@@ -1774,7 +1792,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 const Query<D> qb = active_box<D>(q, amb);   // entries near the re-resolved lanes only
                 bool near = false;
                 const float limw = wave_maxf(amb ? lim : -1.f);
-                if (l < nl) near = gap2_box<D>(qb, tg.tiles[ent].c, tg.tiles[ent].h) <= limw;
+                if (l < nl) near = gap2_box<D>(qb, tg.boxes[ent].c, tg.boxes[ent].h) <= limw;
                 uint64_t em = __ballot(near);
                 while (em) {
                     const int k = __ffsll((unsigned long long)em) - 1;
@@ -2326,11 +2344,12 @@ hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& 
     return hipGetLastError();
 }
 
-hipError_t launch_build_tiles(const double* xyz_in, int dim, int32_t* perm, TileInfo* tiles, int ntiles,
-                              double* xyz64, float4* rel32, int32_t* inv, unsigned* rho_bits, hipStream_t st) {
+hipError_t launch_build_tiles(const double* xyz_in, int dim, int32_t* perm, TileInfo* tiles, TileBox* boxes,
+                              int ntiles, double* xyz64, float4* rel32, int32_t* inv, unsigned* rho_bits,
+                              hipStream_t st) {
     const unsigned g = (unsigned)((ntiles + kWavesPerWG - 1) / kWavesPerWG);
-    hipLaunchKernelGGL(k_build_tiles, dim3(g), dim3(256), 0, st, xyz_in, dim, perm, tiles, ntiles, xyz64, rel32, inv,
-                       rho_bits);
+    hipLaunchKernelGGL(k_build_tiles, dim3(g), dim3(256), 0, st, xyz_in, dim, perm, tiles, boxes, ntiles, xyz64,
+                       rel32, inv, rho_bits);
     return hipGetLastError();
 }
 
