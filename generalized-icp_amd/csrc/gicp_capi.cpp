@@ -817,8 +817,8 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     if (c->use_certs) {
         a.cert_j = c->d_cert_j;
         a.cert_gap = c->d_cert_gap;
-        a.cert_pass = c->d_cert_pass;
     }
+    a.cert_pass = c->d_cert_pass;   // always valid: k_corr reads it (and hint) unconditionally, with the tile metadata
     a.hint = c->d_hint;
     a.partials = c->d_partials;
     a.count_pairs = 1;

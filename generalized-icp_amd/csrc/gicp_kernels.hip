@@ -1203,6 +1203,11 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
     return 1.0;
 }
 
+#ifndef GICP_ROW_SPLIT
+#define GICP_ROW_SPLIT 9
+#endif
+constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
+
 template <int D>
 __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
@@ -1215,10 +1220,46 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     const DevCloud& sc = A.src;
     const DevCloud& tg = A.tgt;
 
-    // pose of this pass from the device state (uniform, scalar loads); converged loops skip -- tested
-    // once the source tile's metadata is requested too, so both round trips overlap
+    // workgroup -> unit (kCorrWaves consecutive source tiles).  Workgroup b runs on XCD b % 8: the
+    // first 8 q8 workgroups are striped so that XCD x walks the contiguous unit range [x q8, x q8 + q8)
+    // in index order (its L2 then holds that region of the target); the remaining units run in index
+    // order.  (Orders that start the previous pass's long units first were measured slower: the
+    // walking set changes from pass to pass, DESIGN.md §3.)
+    const int nunits = (int)gridDim.x, q8 = nunits / 8;
+    int unit = (int)blockIdx.x;
+    if (A.unit_map == 0) {
+        if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
+    } else {   // the k-th workgroup of XCD x takes unit k % C of the XCD's (k / C)-th chunk of C units
+        const int C = A.unit_map, full = nunits / (8 * C) * (8 * C);
+        if (unit < full) unit = (((unit >> 3) / C) * 8 + (unit & 7)) * C + (unit >> 3) % C;
+    }
+    unit = __builtin_amdgcn_readfirstlane(unit);
+    // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
+    int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;
+    if (T >= A.q_end) T = -1;
+    T = __builtin_amdgcn_readfirstlane(T);
+
+    // Everything the wave needs before its first decision, requested in ONE batch of scalar loads (one
+    // memory round trip; a scalar wait covers every load in flight, so a use between them would split
+    // the batch): the pass's pose and convergence flag (device state), the source tile's metadata, the
+    // pass its certificates refer to and last pass's best target tile.  Requested for tile 0 when the
+    // wave has none.  (cert_pass / hint are written only by this wave, at its end; the scalar cache
+    // starts each launch invalidated.)
+    const int Tq = T < 0 ? 0 : T;
     typedef __attribute__((address_space(4))) const IterState* ConstState;
+    typedef __attribute__((address_space(4))) const int32_t* ConstI32;
+    {   // the four array pointers (kernel arguments) in SGPRs first: their loads would otherwise be
+        // interleaved with the batch and each wait for one would wait for the data loads issued before it
+        const void* p0 = A.state;
+        const void* p1 = sc.tiles;
+        const void* p2 = A.cert_pass;
+        const void* p3 = A.hint;
+        asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3));
+    }
     const ConstState cs0 = (ConstState)(uintptr_t)A.state;
+    const TileInfo st = tile_meta(sc, Tq);
+    const int cpass0 = ((ConstI32)(uintptr_t)A.cert_pass)[Tq];
+    const int hint0 = ((ConstI32)(uintptr_t)A.hint)[Tq];
     const bool done = cs0->converged && !A.single_pass;
     struct {
         double R[9], t[3];
@@ -1249,31 +1290,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     }
     for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
     int pairs = 0, list_rebuilds = 0, namb_total = 0, ngproved = 0, nwalked = 0;
-
-    // workgroup -> unit (kCorrWaves consecutive source tiles).  Workgroup b runs on XCD b % 8: the
-    // first 8 q8 workgroups are striped so that XCD x walks the contiguous unit range [x q8, x q8 + q8)
-    // in index order (its L2 then holds that region of the target); the remaining units run in index
-    // order.  (Orders that start the previous pass's long units first were measured slower: the
-    // walking set changes from pass to pass, DESIGN.md §3.)
-    const int nunits = (int)gridDim.x, q8 = nunits / 8;
-    int unit = (int)blockIdx.x;
-    if (A.unit_map == 0) {
-        if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
-    } else {   // the k-th workgroup of XCD x takes unit k % C of the XCD's (k / C)-th chunk of C units
-        const int C = A.unit_map, full = nunits / (8 * C) * (8 * C);
-        if (unit < full) unit = (((unit >> 3) / C) * 8 + (unit & 7)) * C + (unit >> 3) % C;
-    }
-    unit = __builtin_amdgcn_readfirstlane(unit);
-    // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
-    int T = (unit + (unit / kShardChunk) * A.sh_skip + A.sh_first) * kCorrWaves + w;
-    if (T >= A.q_end) T = -1;
     if (T < 0 && done) return;
     if (T >= 0) {
     bool on = false;          // accepted correspondence
     double W[D][D] = {}, sv[D] = {}, wr[D] = {}, rwr = 0.0, r2 = 0.0;
     bool amb = false;
     {
-        const TileInfo st = tile_meta(sc, T);
         if (done) return;
         Query<D> q;
         q.valid = l < st.count;
@@ -1297,7 +1319,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         const bool lists = A.use_lists != 0;
 
         // seed: last pass's best target tile for this source tile, else the Morton neighbour
-        int seed = A.hint ? A.hint[T] : -1;
+        int seed = hint0;
         if (seed < 0 || seed >= tg.ntiles) {
             const uint32_t code = morton_code(q.ow, D, tg.lo, tg.scale, tg.bits);
             int lo = 0, hi = tg.ntiles - 1;
@@ -1347,7 +1369,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (A.cert_j) {
             jp = A.cert_j[i];
             const float g0 = A.cert_gap[i];
-            cdelta = disp_since(A.cert_pass[T]);
+            cdelta = disp_since(cpass0);
             if (cdelta >= 0.f && q.valid) {
                 cj = jp;
                 cgap = g0;
@@ -1409,7 +1431,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     int bk = -1;
 #pragma unroll
                     for (int k = 0; k < kGraphK; ++k) {
-                        if (k == 9) {
+                        if (k == kRowSplit) {
                             asm volatile("" ::: "memory");   // keep the second half's loads here
                             load_half(4);
                         }
@@ -1720,7 +1742,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // that skipped the walk leaves its certificates (and cert_pass) as they are: they stay relative to
         // the older pose, whose direct displacement to later poses is no larger than the summed steps,
         // and the pass writes nothing for it -- until that pose is half the pose ring old.
-        if (A.cert_j && (!skip_walk || any_gcert || A.pass - A.cert_pass[T] >= kPoseRing / 2)) {
+        if (A.cert_j && (!skip_walk || any_gcert || A.pass - cpass0 >= kPoseRing / 2)) {
             if (q.valid) {
                 float g = 0.f;
                 if (gcert) {
