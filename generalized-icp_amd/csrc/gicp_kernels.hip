@@ -465,10 +465,16 @@ struct WaveStage {
 // statistics transpose image of 16 points: u[term][point] and v[term][point], rows padded to 17 doubles
 // (a term's 16 points are written by 16 lanes to consecutive words; the MFMA operand reads of a row
 // group spread over the banks)
+// Only the rows of terms in use are stored (12 u and 10 v terms in 3-D): the MFMA lanes of the unused
+// rows read a duplicate of the last row, whose products land in output rows / columns nobody reads.
+// 22 x 17 doubles (2992 B) instead of 2 x 16 x 17: with the walk's staging (2560 B) in the same union
+// and the wave's statistics written into it after the GEMM, a workgroup takes 12 KB of LDS, 13 per CU
+// instead of 8 -- a CU whose resident workgroups each wait on one long-walking wave can start others.
 constexpr int kStatRow = 17;
+constexpr int kStatU = 12, kStatV = 10;
 struct WaveStat {
-    double u[16 * kStatRow];
-    double v[16 * kStatRow];
+    double u[kStatU * kStatRow];
+    double v[kStatV * kStatRow];
 };
 union __attribute__((aligned(16))) WaveLds {
     WaveStage t;
@@ -1213,7 +1219,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     constexpr int NSX = nstat_ext(D);
     constexpr int NSS = nstat(D);
     __shared__ WaveLds s_lds[kCorrWaves];
-    __shared__ double s_wstat[kCorrWaves][NSX];   // per-wave statistics, accumulated over its tiles
+    // per-wave statistics: written into the wave's own LDS once its statistics GEMM has read it
+    static_assert(sizeof(double) * NSX <= sizeof(WaveLds), "a wave's statistics fit its LDS");
+    auto wstat = [&](int u) -> double* { return reinterpret_cast<double*>(&s_lds[u]); };
 
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     WaveLds& L = s_lds[w];
@@ -1288,7 +1296,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             ring[9 + a] = a < D ? P.t[a] : 0.0;
         }
     }
-    for (int k = l; k < NSX; k += 64) s_wstat[w][k] = 0.0;
     int pairs = 0, list_rebuilds = 0, namb_total = 0, ngproved = 0, nwalked = 0;
     if (T < 0 && done) return;
     if (T >= 0) {
@@ -1975,16 +1982,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         WaveStat& X = s_lds[w].st;
         // points that contribute nothing (rejected, or the tile's padding lanes) have u = 0: a group
         // of 16 or an MFMA's 4 points with none accepted adds exact zeros and is skipped (uniform test)
+        static_assert(NU <= kStatU && NV <= kStatV, "statistics terms fit the transpose image");
         const uint64_t onm = __ballot(on);
         wave_sync();
-        if (onm) {   // the unused term rows read as zeros (this LDS held the walk's staging until now)
-            for (int k = l; k < (16 - NU) * kStatRow; k += 64) X.u[NU * kStatRow + k] = 0.0;
-            for (int k = l; k < (16 - NV) * kStatRow; k += 64) X.v[NV * kStatRow + k] = 0.0;
-        }
         double* const wu = &X.u[l & 15];
         double* const wv = &X.v[l & 15];
-        const double* const ru = &X.u[(l & 15) * kStatRow + (l >> 4)];
-        const double* const rv = &X.v[(l & 15) * kStatRow + (l >> 4)];
+        const double* const ru = &X.u[min(l & 15, NU - 1) * kStatRow + (l >> 4)];
+        const double* const rv = &X.v[min(l & 15, NV - 1) * kStatRow + (l >> 4)];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (((onm >> (16 * g)) & 0xFFFFull) == 0) continue;
@@ -2002,7 +2006,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
             wave_sync();
         }
-        // lane l holds stats[p = (l>>4) + 4j][q = l&15], j = 0..3
+        // lane l holds stats[p = (l>>4) + 4j][q = l&15], j = 0..3; the GEMM's operands are read, so the
+        // wave's statistics now overwrite its LDS: zeros, then each statistic from its owner lane
+        double* const wst = wstat(w);
+        for (int k = l; k < NSX; k += 64) wst[k] = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int p = (l >> 4) + 4 * j, qq = l & 15;
@@ -2019,17 +2026,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             } else if (qq == NS + D && p == NS + D + 2) {
                 idx = NSS + 3;                                            // sum |r|^2
             }
-            if (idx >= 0) s_wstat[w][idx] += acc[j];   // each (p,q) has one owner lane: no race
+            if (idx >= 0) wst[idx] = acc[j];   // each (p,q) has one owner lane: no race
         }
         namb_total += (int)__popcll(__ballot(amb));
     }
-    }   // the wave's tile
+    } else {   // no tile: zeros
+        for (int k = l; k < NSX; k += 64) wstat(w)[k] = 0.0;
+    }
     if (l == 0) {
-        s_wstat[w][NSS] = (double)namb_total;
-        s_wstat[w][NSS + 1] = (double)pairs * 64.0;
-        s_wstat[w][NSS + 2] = (double)list_rebuilds;
-        s_wstat[w][NSS + 4] = (double)ngproved;
-        s_wstat[w][NSS + 5] = (double)nwalked;
+        double* const wst = wstat(w);
+        wst[NSS] = (double)namb_total;
+        wst[NSS + 1] = (double)pairs * 64.0;
+        wst[NSS + 2] = (double)list_rebuilds;
+        wst[NSS + 4] = (double)ngproved;
+        wst[NSS + 5] = (double)nwalked;
     }
     S.mark(6);
 #if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
@@ -2060,7 +2070,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) {
         double s = 0.0;
 #pragma unroll
-        for (int u = 0; u < kCorrWaves; ++u) s += s_wstat[u][t];
+        for (int u = 0; u < kCorrWaves; ++u) s += wstat(u)[t];
         __hip_atomic_store(&A.partials[(int64_t)unit * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
