@@ -1460,8 +1460,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                             bx = dx;
                             by = dy;
                             bz = dz;
-                        } else {
-                            b2 = fminf(b2, dd);
+                        } else {   // (non-negative floats order like their bits: v_min_u32, no NaN canonicalisation)
+                            b2 = __uint_as_float(min(__float_as_uint(b2), __float_as_uint(dd)));
                         }
                     }
                     const float d0 = __builtin_amdgcn_sqrtf(d0s);
