@@ -2094,7 +2094,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     double (*s_red)[NSX] = reinterpret_cast<double (*)[NSX]>(&s_lds[0]);
     double* s_sum = reinterpret_cast<double*>(&s_lds[0]) + 3 * NSX;
     auto sum_rows = [&](const double* src, int b0, int b1, double* dst_stat) {
-        constexpr int PART = 22;                                  // rows per thread per chunk
+        constexpr int PART = 27;   // rows per thread per chunk: 3 x 27 = 81 covers a 64-unit group and the 79 groups of 1M in one round trip
         constexpr int NP = (64 * kCorrWaves) / NSX >= 3 ? 3 : 1;  // threads per statistic
         constexpr int NT = 64 * kCorrWaves;
         const int tid = threadIdx.x;
