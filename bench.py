@@ -75,6 +75,12 @@ def parse():
     ap.add_argument("--shard-index", type=int, default=0, help="diagnostic: which shard --shard-sim runs")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks (gloo, CPU only) and report RANK / WORLD_SIZE; no GPU work")
+    ap.add_argument("--exchange", choices=("peer", "rccl"), default="peer",
+                    help="N > 1: the statistics exchange -- 'peer' (in-kernel, IPC-mapped areas; falls back to "
+                         "RCCL when its probe fails on any rank) or 'rccl' (ncclAllReduce + k_solve)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="diagnostic: the N ranks share GPU 0 (peer exchange only; RCCL refuses); times the "
+                         "protocol, not a multi-GPU job")
     return ap.parse_args()
 
 
@@ -89,7 +95,7 @@ def launch_ranks(a):
     """--gpus N > 1 without a launcher: N rank processes under torch.distributed.run, as CHILD
     processes (never exec: nothing here has touched the GPU, and nothing may before the ranks do).
     Returns the exit status to leave with."""
-    if not a.dry_run:
+    if not a.dry_run and not a.share_gpu:
         import torch
         ngpu = torch.cuda.device_count()   # counts devices without initialising HIP on this image
         if ngpu < a.gpus:
@@ -188,25 +194,34 @@ def main():
         dry_run(world, rank, local)
         return
     dist = None
+    dev = 0 if a.share_gpu else local
+    if a.share_gpu and a.exchange != "peer":
+        raise SystemExit("bench.py: --share-gpu needs --exchange peer (RCCL refuses two ranks on one GPU)")
     if world > 1:
         import torch
         import torch.distributed as dist
-        if local >= torch.cuda.device_count():   # RCCL refuses two ranks on one GPU
+        if dev >= torch.cuda.device_count():   # RCCL refuses two ranks on one GPU
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {torch.cuda.device_count()} GPUs")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo" if a.share_gpu else "nccl")
     import gicp
+    from gicp import distributed as gd
 
     src, tgt, Tgt, kw, name = workload(a.n, a.dim)
     params = gicp.default_params(a.dim, fixed_iterations=1, **kw)
-    eng = gicp.Engine(local)
+    eng = gicp.Engine(dev)
+    peer_note = None
     if world > 1:
-        uid = [gicp.Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(world, rank, uid[0])
+        if a.exchange == "peer":
+            peer_note = gd.init_peer(eng, rank, world)
+        if a.exchange == "rccl" or peer_note is not None:   # asked for, or the peer probe failed on some rank
+            if a.share_gpu:
+                raise SystemExit(f"rank {rank}: the peer exchange failed on one GPU: {peer_note}")
+            gd.init_comm(eng, rank, world)
     comm_ranks, _, comm_kind = eng.comm_ranks()
-    if world > 1 and (comm_ranks != world or comm_kind != "rccl"):
-        raise SystemExit(f"rank {rank}: the RCCL communicator reports {comm_ranks} ranks ({comm_kind}), expected {world}")
+    want = "peer" if (a.exchange == "peer" and peer_note is None) else "rccl"
+    if world > 1 and (comm_ranks != world or comm_kind != want):
+        raise SystemExit(f"rank {rank}: the exchange reports {comm_ranks} ranks ({comm_kind}), expected {world} ({want})")
     t0 = time.perf_counter()
     eng.set_target(tgt, params)
     if world == 1 and a.shard_sim > 1:
@@ -220,6 +235,7 @@ def main():
             import torch
             dist.barrier()
             torch.cuda.synchronize()
+            dist.barrier()
 
     params.max_iterations = max(1, a.warmup)
     eng.align(None, params)
@@ -264,7 +280,7 @@ def main():
     if dist is not None:
         import torch
         t = torch.tensor([elapsed, corr_ms_total, warm_elapsed or 0.0, *per_iter], dtype=torch.float64,
-                         device=f"cuda:{local}")
+                         device="cpu" if a.share_gpu else f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, corr_ms_total = float(t[0]), float(t[1])
         warm_elapsed = float(t[2]) or None
@@ -301,10 +317,13 @@ def main():
                  else "synthetic (2-D segment scene of BASELINE.md §3, 0.5 px noise)"),
         "config": {"workload": name, "n_source": a.n, "n_target": a.n, "dim": a.dim,
                    "k": 20 if a.dim == 3 else 6, **kw,
-                   "parallelism": f"dp{world} (source shards; RCCL all-reduce of {stats_exchanged(a.dim)} fp64 "
-                                  f"per iteration)" if world > 1 else "dp1 (one GPU, no collective)"},
+                   "parallelism": (f"dp{world} (source shards; {stats_exchanged(a.dim)} fp64 per iteration summed "
+                                   + ("in-kernel over IPC-mapped peer areas, the solve in the same launch)"
+                                      if comm_kind == "peer" else "by RCCL all-reduce, then k_solve)"))
+                   if world > 1 else "dp1 (one GPU, no collective)"},
         "comm_ranks": comm_ranks,
         "comm": comm_kind,
+        "comm_fallback": peer_note,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "traffic_per_pass": None if not traffic_pp else
@@ -318,9 +337,11 @@ def main():
                      "impl_frac": impl_bytes / (corr_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_timing": "HIP events, every k_corr launch of K timed once (8 identical cold-start "
                                       "K-iteration runs at sampling offsets 0..7, stride 8)",
-                     "kernel_note": ("k_corr's final workgroup also runs the one-wave inner solve and pose update "
-                                     "(~5 us, inside the timed duration)" if world == 1 and a.shard_sim <= 1 else
-                                     "the inner solve is k_solve after the statistics exchange (not in k_corr's time)")},
+                     "kernel_note": ("the inner solve is k_solve after the RCCL all-reduce (not in k_corr's time)"
+                                     if comm_kind == "rccl" else
+                                     "k_corr's final workgroup also runs the one-wave inner solve and pose update "
+                                     "(~5 us, inside the timed duration)" +
+                                     (", after the in-kernel peer exchange" if comm_kind == "peer" else ""))},
         "passes": {"moving_pass_us": float(np.mean(per_iter[:n_mov])) * 1e3,
                    "converged_pass_us": float(np.mean(per_iter[-n_mov:])) * 1e3,
                    "first_pass_us": float(per_iter[0]) * 1e3,
@@ -338,8 +359,13 @@ def main():
         "correspondences": res["correspondences"],
         "ambiguous_last_pass": res["ambiguous"],
     }
+    if a.share_gpu:
+        line["diagnostic"] = f"{world} ranks sharing GPU 0 (peer exchange protocol timing, not a multi-GPU job)"
+        line["cpu_baseline"] = None
+        print(json.dumps(line))
+        return
     if a.shard_sim > 1 and world == 1:
-        line["diagnostic"] = f"shard {a.shard_index} of {a.shard_sim} only, no all-reduce: one rank of a {a.shard_sim}-GPU job"
+        line["diagnostic"] = f"shard {a.shard_index} of {a.shard_sim} only, no exchange: one rank of a {a.shard_sim}-GPU job"
         line["cpu_baseline"] = None
         print(json.dumps(line))
         return

@@ -36,6 +36,7 @@ hipError_t launch_build_blocks(const TileInfo*, int, BlockInfo*, int, int, hipSt
 hipError_t launch_knn_cov(const CovArgs&, int, int, bool, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t, double*);
+hipError_t launch_peer_probe(const PeerArgs&, double*, hipStream_t);
 hipError_t launch_graph_pack(const GraphArgs&, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
@@ -352,6 +353,14 @@ struct gicp_ctx {
     gicp_allreduce_fn hook = nullptr;  // host statistics exchange (gicp_set_allreduce)
     void* hook_user = nullptr;
     double* h_xchg = nullptr;         // pinned exchange buffer of the hook
+    // in-kernel peer exchange (gicp_peer_export / gicp_peer_init)
+    double* d_peer_area = nullptr;    // this rank's exchange area (uncached device memory, IPC-exported)
+    void* peer_open[kMaxPeers] = {};  // the peers' areas as opened here (closed by gicp_peer_close)
+    PeerArgs peer{};                  // n > 1 while the peer exchange is on
+    uint64_t peer_seq = 0;            // sequence number of the last exchange launch (the same on every rank)
+    double peer_timeout_s = 10.0;
+    double* d_probe = nullptr;
+    double** d_peer_ptrs = nullptr;   // device copy of the areas' addresses (PeerArgs::area)
     std::vector<float> iter_ms;       // sampled k_corr time per iteration of the last align (-1: not sampled)
     double* d_rot = nullptr;          // gicp_rotated_covariances output
     size_t cap_rot = 0;
@@ -835,11 +844,16 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.gap_slack = (float)std::ldexp(std::sqrt((double)a.search2) + 2.0 * c->tgt.rho + 2.0 * c->src.rho, -19);
     a.cov_model = c->psrc.cov_model;
     a.pl_inv = 1.0 / (c->ptgt.epsilon * (1.0 - c->ptgt.ratio));   // target m = sqrt(eps (1 - ratio)) n
+    if (c->peer.n > 1) {   // every launch is an exchange: ranks count launches alike (same calls, same order)
+        a.peer = c->peer;
+        a.peer.seq = ++c->peer_seq;
+    }
     return a;
 }
 
 void allreduce_stats(gicp_ctx* c) {
     const int nsx = nstat_ext(c->src.dim);
+    if (c->peer.n > 1) return;   // summed inside k_corr
     if (c->hook) {   // host exchange: statistics out, the caller's sum over ranks back in
         HIPCHK(hipMemcpyAsync(c->h_xchg, c->d_state->stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -981,8 +995,14 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
     HIPCHK(hipMemsetAsync(d_stamps, 0, nst * 8, st));
     a.stamps = d_stamps;
 #endif
-    if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
-    else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nsx, st));
+    if (grid > 0) {
+        HIPCHK(launch_corr(a, d, grid, st));
+    } else if (a.peer.n > 1) {   // no tile in this shard: one empty workgroup still takes part in the exchange
+        a.q_end = 0;
+        HIPCHK(launch_corr(a, d, 1, st));
+    } else {
+        HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nsx, st));
+    }
     allreduce_stats(c);
     HIPCHK(hipMemcpyAsync(c->h_stats, c->d_state->stats, sizeof(double) * nsx, hipMemcpyDeviceToHost, st));
     c->top_cached_k = 0;
@@ -999,6 +1019,11 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
             HIPCHK(hipMemcpyAsync(dbg->distance, c->d_dbg_dist, sizeof(double) * n, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    if (a.peer.n > 1) {
+        int fail = 0;
+        HIPCHK(hipMemcpy(&fail, &c->d_state->solve_fail, sizeof(int), hipMemcpyDeviceToHost));
+        if (fail == 2) throw Fail{GICP_E_COMM, "peer exchange timed out (a rank did not arrive)"};
+    }
 #if defined(GICP_STAMPS) || defined(GICP_TIMELINE)
     print_stamps(d_stamps, nst);
 #endif
@@ -1015,6 +1040,18 @@ void run_pass(gicp_ctx* c, const double* T, gicp_debug* dbg) {
 }  // namespace
 
 namespace {
+// drop the peer exchange: unmap the peers' areas (this rank's own area stays, re-exportable)
+void close_peers(gicp_ctx* c) {
+    bool any = c->peer.n > 1;
+    for (void* p : c->peer_open) any = any || p != nullptr;
+    if (any) (void)hipStreamSynchronize(c->stream);   // no launch of ours still uses the mappings
+    for (auto& p : c->peer_open) {
+        if (p) (void)hipIpcCloseMemHandle(p);
+        p = nullptr;
+    }
+    c->peer = PeerArgs{};
+}
+
 int guard_impl(gicp_ctx* c, const char* where, const std::function<void()>& body) {
     try {
         if (c) HIPCHK(hipSetDevice(c->device));
@@ -1099,6 +1136,11 @@ void gicp_destroy(gicp_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    for (auto& p : c->peer_open)
+        if (p) (void)hipIpcCloseMemHandle(p);
+    if (c->d_peer_area) (void)hipFree(c->d_peer_area);
+    dfree(c->d_probe);
+    dfree(c->d_peer_ptrs);
     c->tgt.release();
     c->src.release();
     dfree(c->d_hint);
@@ -1160,6 +1202,7 @@ int gicp_comm_init(gicp_ctx* c, int nranks, int rank, const char id[GICP_COMM_ID
             c->comm = nullptr;
         }
         c->hook = nullptr;   // one exchange per context
+        close_peers(c);
         // a one-rank communicator is created too: the all-reduce then runs (as an identity) on the
         // same stream path as a multi-GPU job, which is how the one-GPU tests exercise it
         ncclUniqueId uid;
@@ -1175,7 +1218,11 @@ int gicp_comm_ranks(gicp_ctx* c, int* nranks, int* rank, int* kind) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_comm_ranks", [&] {
         int n = 1, r = 0, k = 0;
-        if (c->comm) {
+        if (c->peer.n > 1) {
+            n = c->peer.n;
+            r = c->peer.rank;
+            k = 3;
+        } else if (c->comm) {
             ncclResult_t e = ncclCommCount(c->comm, &n);
             if (e == ncclSuccess) e = ncclCommUserRank(c->comm, &r);
             if (e != ncclSuccess) throw Fail{GICP_E_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(e)};
@@ -1412,9 +1459,12 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                     a.dbg_det = c->d_dbg_det;
                     a.top_tgt = c->d_top_tgt;
                 }
-                // one unsharded rank (no exchange of the statistics): k_corr's final workgroup runs the solve too
-                // (a shard without a communicator -- bench.py --shard-sim -- keeps the multi-rank launch shape)
-                const bool fuse = c->fuse_solve && grid > 0 && !c->hook && !c->comm && c->nshards == 1;
+                // k_corr's final workgroup runs the solve too whenever it holds the sums the solve needs: with
+                // no exchange (one rank, or bench.py --shard-sim's lone shard: the peer-exchange launch shape
+                // without the exchange) and with the in-kernel peer exchange; RCCL and the host hook sit
+                // between k_corr and k_solve
+                const bool peer = a.peer.n > 1;
+                const bool fuse = c->fuse_solve && (peer || (grid > 0 && !c->hook && !c->comm));
                 double* const hist = trace ? c->d_hist + (size_t)it * HS : nullptr;
                 if (fuse) {
                     a.fuse_solve = 1;
@@ -1422,8 +1472,14 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                 }
                 const bool ev = timing && it % kEvStride == kEvOffset;
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b], st));
-                if (grid > 0) HIPCHK(launch_corr(a, d, grid, st));
-                else HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nstat_ext(d), st));
+                if (grid > 0) {
+                    HIPCHK(launch_corr(a, d, grid, st));
+                } else if (peer) {   // no tile in this shard: one empty workgroup takes part in the exchange
+                    a.q_end = 0;
+                    HIPCHK(launch_corr(a, d, 1, st));
+                } else {
+                    HIPCHK(hipMemsetAsync(c->d_state->stats, 0, sizeof(double) * nstat_ext(d), st));
+                }
                 if (ev) HIPCHK(hipEventRecord(c->ev[2 * b + 1], st));
                 if (tk > 0)   // launched after convergence too (the pass exited at once): rows >= iter are ignored
                     HIPCHK(launch_top_weights(c->d_dbg_det, c->d_top_tgt, c->src.perm, c->src.n, tk, c->d_top_v,
@@ -1475,6 +1531,7 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                 }
             }
         }
+        if (hs.solve_fail == 2) throw Fail{GICP_E_COMM, "peer exchange timed out (a rank did not arrive)"};
         if (hs.solve_fail) throw Fail{GICP_E_INVALID, "pose solve failed (degenerate statistics)"};
         std::memcpy(T_out, hs.T, sizeof(double) * n1 * n1);
         if (res) {
@@ -1528,13 +1585,25 @@ int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const 
         }
         g.rc = GICP_OK;
         g.err.clear();
+        // the caller's scan is copied into the slot's pinned buffer before this call returns (the caller
+        // may refill its buffer at once): 16 fixed chunks on the calling thread's tiling pool (a 100k-point
+        // frame, 2.4 MB, in ~0.1 ms instead of one thread's ~0.3 ms)
+        {
+            const size_t total = sizeof(double) * need;
+            char* dst = reinterpret_cast<char*>(g.bs.h_pinned);
+            const char* srcb = reinterpret_cast<const char*>(xyz);
+            constexpr int kChunks = 16;
+            c->bs.workers().run(kChunks, [&](int k) {
+                const size_t b0 = total * k / kChunks, b1 = total * (k + 1) / kChunks;
+                std::memcpy(dst + b0, srcb + b0, b1 - b0);
+            });
+        }
         const bool graph = c->use_graph && c->use_certs;
         const int dev = c->device;
         gicp_ctx::Staged* gp = &g;
-        g.th = std::thread([gp, xyz, M, dim, graph, dev] {
+        g.th = std::thread([gp, M, dim, graph, dev] {
             try {
                 HIPCHK(hipSetDevice(dev));
-                std::memcpy(gp->bs.h_pinned, xyz, sizeof(double) * (size_t)M * dim);
                 build_cloud(gp->cl, gp->bs.h_pinned, M, dim, gp->p, graph, gp->bs, gp->stream, true);
             } catch (const Fail& f) {
                 gp->rc = f.code;
@@ -1602,8 +1671,13 @@ int gicp_iteration_times(gicp_ctx* c, float* out, int n) {
 }
 
 int gicp_set_allreduce(gicp_ctx* c, gicp_allreduce_fn fn, void* user) {
-    if (!c) return GICP_E_INVALID;
+    return gicp_set_allreduce_ranks(c, fn, user, 1, 0);
+}
+
+int gicp_set_allreduce_ranks(gicp_ctx* c, gicp_allreduce_fn fn, void* user, int nranks, int rank) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return GICP_E_INVALID;
     return guard_impl(c, "gicp_set_allreduce", [&] {
+        if (fn) close_peers(c);
         if (fn && !c->h_xchg) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_xchg), sizeof(double) * 80));
         if (fn && c->comm) {   // one exchange per context: the hook replaces the communicator
             HIPCHK(hipStreamSynchronize(c->stream));
@@ -1612,7 +1686,102 @@ int gicp_set_allreduce(gicp_ctx* c, gicp_allreduce_fn fn, void* user) {
         }
         c->hook = fn;
         c->hook_user = fn ? user : nullptr;
+        if (!c->comm) {   // what gicp_comm_ranks reports for the hook
+            c->nranks = fn ? nranks : 1;
+            c->rank = fn ? rank : 0;
+        }
     });
+}
+
+int gicp_peer_export(gicp_ctx* c, char handle[GICP_PEER_HANDLE_BYTES]) {
+    if (!c || !handle) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_peer_export", [&] {
+        static_assert(sizeof(hipIpcMemHandle_t) == GICP_PEER_HANDLE_BYTES, "IPC handle size");
+        if (!c->d_peer_area) {   // uncached: peers' stores and this rank's polling meet in memory
+            HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->d_peer_area), sizeof(double) * kPeerAreaDoubles,
+                                         hipDeviceMallocUncached));
+            HIPCHK(hipMemset(c->d_peer_area, 0, sizeof(double) * kPeerAreaDoubles));
+            HIPCHK(hipDeviceSynchronize());
+        }
+        hipIpcMemHandle_t h;
+        HIPCHK(hipIpcGetMemHandle(&h, c->d_peer_area));
+        std::memcpy(handle, &h, sizeof(h));
+    });
+}
+
+int gicp_peer_init(gicp_ctx* c, int nranks, int rank, const char* handles, double timeout_s) {
+    if (!c || !handles || nranks < 2 || nranks > GICP_MAX_PEERS || rank < 0 || rank >= nranks || !(timeout_s > 0.0))
+        return GICP_E_INVALID;
+    return guard_impl(c, "gicp_peer_init", [&] {
+        if (!c->d_peer_area) throw Fail{GICP_E_STATE, "gicp_peer_export first"};
+        close_peers(c);
+        PeerArgs p{};
+        p.n = nranks;
+        p.rank = rank;
+        p.own = c->d_peer_area;
+        double* area[kMaxPeers] = {};
+        try {
+            for (int r = 0; r < nranks; ++r) {
+                if (r == rank) {
+                    area[r] = c->d_peer_area;
+                    continue;
+                }
+                hipIpcMemHandle_t h;
+                std::memcpy(&h, handles + (size_t)r * GICP_PEER_HANDLE_BYTES, sizeof(h));
+                void* ptr = nullptr;
+                const hipError_t e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
+                if (e != hipSuccess)
+                    throw Fail{GICP_E_COMM, std::string("hipIpcOpenMemHandle(rank ") + std::to_string(r) + "): " +
+                                                hipGetErrorString(e)};
+                c->peer_open[r] = ptr;
+                area[r] = static_cast<double*>(ptr);
+            }
+            if (!c->d_peer_ptrs) dalloc(c->d_peer_ptrs, kMaxPeers);
+            HIPCHK(hipMemcpy(c->d_peer_ptrs, area, sizeof(area), hipMemcpyHostToDevice));
+            p.area = c->d_peer_ptrs;
+            int khz = 0;
+            HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+            p.timeout = (uint64_t)(timeout_s * (khz > 0 ? khz : 100000) * 1e3);
+            // the probe: one exchange of (rank + 1, 1), which every rank runs now
+            if (!c->d_probe) dalloc(c->d_probe, 2);
+            p.seq = ++c->peer_seq;
+            HIPCHK(launch_peer_probe(p, c->d_probe, c->stream));
+            double got[2] = {0, 0};
+            HIPCHK(hipMemcpyAsync(got, c->d_probe, sizeof(got), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (got[0] != 0.5 * nranks * (nranks + 1) || got[1] != (double)nranks)
+                throw Fail{GICP_E_COMM, "peer exchange probe failed (got " + std::to_string(got[0]) + ", " +
+                                            std::to_string(got[1]) + ")"};
+        } catch (...) {
+            close_peers(c);
+            throw;
+        }
+        // the peer exchange replaces any other exchange of this context
+        if (c->comm) {
+            ncclCommDestroy(c->comm);
+            c->comm = nullptr;
+        }
+        c->hook = nullptr;
+        c->peer = p;
+        c->peer_timeout_s = timeout_s;
+        c->nranks = nranks;
+        c->rank = rank;
+    });
+}
+
+int gicp_peer_close(gicp_ctx* c) {
+    if (!c) return GICP_E_INVALID;
+    return guard_impl(c, "gicp_peer_close", [&] { close_peers(c); });
+}
+
+const char* gicp_build_info(void) {
+#ifndef GICP_SRC_HASH
+#define GICP_SRC_HASH "unknown"
+#endif
+#ifndef GICP_GIT_REV
+#define GICP_GIT_REV "unknown"
+#endif
+    return "src=" GICP_SRC_HASH ";git=" GICP_GIT_REV ";built=" __DATE__ " " __TIME__ ";arch=gfx950";
 }
 
 int gicp_rotated_covariances(gicp_ctx* c, int which, const double* R, double* out) {

@@ -58,7 +58,9 @@ struct __attribute__((aligned(16))) TileInfo {
 struct __attribute__((aligned(16))) TileBox {
     double c[3];      // = TileInfo::c
     float h[3];       // = TileInfo::h
-    uint32_t sc6;     // (start << 6) | (count - 1)   (gicp_set_* keep n < 2^26)
+    int32_t start;    // = TileInfo::start (any n < 2^31)
+    int32_t count;    // = TileInfo::count
+    int32_t pad;
 };
 static_assert(sizeof(TileBox) == 48, "TileBox is three 16-B words");
 
@@ -172,6 +174,26 @@ constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
 constexpr int kShardChunk = 16;
 constexpr int kMaxGroups = 4096;   // ticket counters available
 
+// In-kernel peer exchange of the statistics (include/gicp_hip.h gicp_peer_init).  Each rank
+// owns an exchange area in fine-grained (uncached) device memory, mapped into every peer by IPC:
+//   uint64 flag[2][kMaxPeers]              sequence number of the launch whose slot last arrived
+//   double slot[2][kMaxPeers][kPeerSlot]   rank p's statistics of that launch
+// indexed [parity of the launch's sequence number][sending rank].  Two parities suffice: a rank writes
+// launch s + 1's slot only after its launch s read every slot of s (stream order), and launch s + 2's
+// only after every rank wrote s + 1's, i.e. after every rank finished reading s.
+constexpr int kMaxPeers = GICP_MAX_PEERS;
+constexpr int kPeerSlot = 80;
+constexpr int kPeerFlagWords = 2 * kMaxPeers;   // doubles before the slots
+constexpr size_t kPeerAreaDoubles = kPeerFlagWords + (size_t)2 * kMaxPeers * kPeerSlot;
+struct PeerArgs {
+    double* const* area;       // device array [n]: rank p's area as mapped here (area[rank] = this rank's own)
+    double* own;               // = area[rank]
+    int32_t n;                 // ranks (0: no peer exchange)
+    int32_t rank;
+    uint64_t seq;              // this launch's sequence number (>= 1, the same on every rank)
+    uint64_t timeout;          // wall-clock ticks (wall_clock64) a rank waits for its peers
+};
+
 struct CorrArgs {
     DevCloud src, tgt;
     int32_t q_begin, q_end;   // k_corr: q_begin unused (0), q_end = the cloud's tile count
@@ -225,6 +247,7 @@ struct CorrArgs {
     // of the statistics between ranks comes between them; `hist` = this iteration's gicp_trace row or null
     int32_t fuse_solve;
     double* hist;
+    PeerArgs peer;            // n > 1: the final workgroup exchanges the statistics with its peers in-kernel
 };
 
 constexpr int nstat(int D) {

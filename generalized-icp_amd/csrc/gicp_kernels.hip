@@ -289,7 +289,9 @@ __global__ void __launch_bounds__(256) k_build_tiles(const double* __restrict__ 
             b.c[a] = c[a];
             b.h[a] = h[a];
         }
-        b.sc6 = ((uint32_t)start << 6) | (uint32_t)(count - 1);
+        b.start = start;
+        b.count = count;
+        b.pad = 0;
         atomicMax(rho_bits, __float_as_uint(rad));
     }
 }
@@ -594,12 +596,13 @@ __device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, in
                 const int t = first + l;
                 bool ct = false;
                 float g2 = 3e38f;
-                uint32_t sc6 = 0;   // (start << 6) | (count - 1)
+                int tst = 0, tcnt = 0;   // the tile's start, count
                 if (l < nt && t != seed) {
                     const TileBox tb = db.boxes[t];
                     g2 = gap2_box<D>(q, tb.c, tb.h);
                     ct = g2 <= wbi;
-                    sc6 = tb.sc6;
+                    tst = tb.start;
+                    tcnt = tb.count;
                 }
                 if (skin > 0.f) {
                     uint64_t cm = __ballot(ct);
@@ -611,8 +614,7 @@ __device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, in
                 uint64_t tm = __ballot(g2 <= wb);
                 auto pick = [&]() -> int { return tm ? __ffsll((unsigned long long)tm) - 1 : -1; };
                 auto coords = [&](int kk) {
-                    const uint32_t v = __builtin_amdgcn_readlane(sc6, kk);
-                    return load_rel(db, (int)(v >> 6), (int)(v & 63u) + 1);
+                    return load_rel(db, __builtin_amdgcn_readlane(tst, kk), __builtin_amdgcn_readlane(tcnt, kk));
                 };
                 for (int k = pick(); k >= 0; k = pick()) {
                     tm &= ~(1ull << k);
@@ -1214,6 +1216,69 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 #endif
 constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
 
+// In-kernel exchange of a workgroup's NV values with every peer rank (PeerArgs, gicp_internal.h), called by
+// all threads of one workgroup: `vals` (LDS) goes into this rank's slot of every rank's area, then the
+// launch's sequence number into the flags; the workgroup waits until every rank's flag of this launch has
+// arrived in its own area (at most P.timeout wall-clock ticks: a missing peer fails the exchange, it never
+// hangs the launch) and replaces `vals` by the sum over ranks in rank order -- the same bits on every
+// rank.  Returns false on a timeout (uniform over the workgroup).  System-scope stores and a system
+// release before the flags; acquire loads on the flags; the areas are uncached device memory.
+template <int NV>
+__device__ bool peer_exchange(const PeerArgs P, double* vals) {   // (by value: a reference into the kernel
+                                                                  // arguments made them a scratch copy)
+    static_assert(NV <= kPeerSlot, "an exchange slot holds the values");
+    __shared__ int s_fail;
+    const int R = P.n, me = P.rank, tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    const int par = (int)(P.seq & 1u);
+    for (int p = 0; p < R; ++p) {   // (p uniform: one scalar load of each peer's pointer)
+        double* const dst = P.area[p] + kPeerFlagWords + (size_t)(par * kMaxPeers + me) * kPeerSlot;
+        for (int k = tid; k < NV; k += nt) __hip_atomic_store(dst + k, vals[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __threadfence_system();   // this thread's slot stores complete and visible system-wide
+    if (tid == 0) s_fail = 0;
+    __syncthreads();          // ... every thread's, before any flag
+    if (tid < R) {
+        uint64_t* f = reinterpret_cast<uint64_t*>(P.area[tid]) + par * kMaxPeers + me;
+        __hip_atomic_store(f, P.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t* g = reinterpret_cast<const uint64_t*>(P.own) + par * kMaxPeers + tid;
+        const uint64_t t0 = (uint64_t)wall_clock64();
+        while (__hip_atomic_load(g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != P.seq) {
+            if ((uint64_t)wall_clock64() - t0 > P.timeout) {
+                s_fail = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    if (s_fail) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // every thread: the peers' slots after their flags
+    for (int k = tid; k < NV; k += nt) {
+        double s = 0.0;
+        for (int p = 0; p < R; ++p)
+            s += __hip_atomic_load(P.own + kPeerFlagWords + (size_t)(par * kMaxPeers + p) * kPeerSlot + k,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        vals[k] = s;
+    }
+    __syncthreads();
+    return true;
+}
+
+// gicp_peer_init's probe: one exchange of (rank + 1, 1) -> out = (sum, ranks), or (-1, -1) on a timeout
+__global__ void __launch_bounds__(64) k_peer_probe(PeerArgs P, double* out) {
+    __shared__ double v[2];
+    if (threadIdx.x == 0) {
+        v[0] = (double)(P.rank + 1);
+        v[1] = 1.0;
+    }
+    __syncthreads();
+    const bool ok = peer_exchange<2>(P, v);
+    if (threadIdx.x == 0) {
+        out[0] = ok ? v[0] : -1.0;
+        out[1] = ok ? v[1] : -1.0;
+    }
+}
+
 template <int D>
 __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArgs A) {
     constexpr int NSX = nstat_ext(D);
@@ -1616,7 +1681,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             S.mark(3);
             return true;
         };
-        auto visit = [&](int Tt) -> bool { return visit_pre(Tt, nullptr); };
         S.mark(0);
         // candidate list of this source tile: usable if built within the pose ring and the tile's
         // displacement since then is inside the certified radius
@@ -2155,6 +2219,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     double hv = 0.0;
     if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     sum_rows(A.gpart, 0, ng, s_sum);
+    if (A.peer.n > 1 && !peer_exchange<NSX>(A.peer, s_sum)) {   // the sum over ranks, in-kernel
+        if (threadIdx.x == 0) {   // a peer never arrived: fail the call, later launches exit at once
+            A.state->solve_fail = 2;
+            A.state->converged = 1;
+            __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!fuse || threadIdx.x >= 64) return;
@@ -2438,6 +2510,11 @@ hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
     if (grid <= 0) return hipSuccess;
     if (dim == 2) hipLaunchKernelGGL(k_corr<2>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
     else hipLaunchKernelGGL(k_corr<3>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_peer_probe(const PeerArgs& p, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, st, p, out);
     return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ class Engine:
         self.generation = 0        # bumped whenever the source cloud changes (lazy covariance views)
         self._staged = []          # (array, params) of the staged targets, oldest first: kept alive until committed
         self._hook = None          # keeps the ctypes callback of set_allreduce alive
+        self._hook_fn = None       # (fn, nranks, rank) of that hook, to restore it after a gicp() call
 
     def close(self):
         if self._ctx:
@@ -142,7 +143,26 @@ class Engine:
         (gicp_comm_ranks); kind is 'none', 'rccl' or 'hook'."""
         n, r, k = C.c_int(), C.c_int(), C.c_int()
         check(self._lib.gicp_comm_ranks(self._ctx, C.byref(n), C.byref(r), C.byref(k)), self._ctx, "gicp_comm_ranks")
-        return n.value, r.value, {0: "none", 1: "rccl", 2: "hook"}[k.value]
+        return n.value, r.value, {0: "none", 1: "rccl", 2: "hook", 3: "peer"}[k.value]
+
+    def peer_export(self) -> bytes:
+        """This rank's exchange area as an IPC handle (gicp_peer_export): all-gather it, then peer_init."""
+        buf = C.create_string_buffer(_lib.PEER_HANDLE_BYTES)
+        check(self._lib.gicp_peer_export(self._ctx, buf), self._ctx, "gicp_peer_export")
+        return buf.raw
+
+    def peer_init(self, nranks, rank, handles, timeout=10.0):
+        """Map the peers' exchange areas (handles in rank order) and prove the path with one probe
+        exchange (gicp_peer_init, collective): from then on every pass sums the statistics over the
+        ranks inside its own launch.  Raises GicpError (code GICP_E_COMM) when the path does not work."""
+        if len(handles) != nranks or any(len(h) != _lib.PEER_HANDLE_BYTES for h in handles):
+            raise ValueError(f"need {nranks} handles of {_lib.PEER_HANDLE_BYTES} bytes")
+        blob = b"".join(handles)
+        check(self._lib.gicp_peer_init(self._ctx, int(nranks), int(rank), blob, float(timeout)), self._ctx,
+              "gicp_peer_init")
+
+    def peer_close(self):
+        check(self._lib.gicp_peer_close(self._ctx), self._ctx, "gicp_peer_close")
 
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -176,12 +196,12 @@ class Engine:
     def stage_target(self, pts, params=None):
         """Build `pts` as a coming target on its own stream while the current one is registered
         (gicp_stage_target; up to MAX_STAGED pending); commit_target makes the oldest current.  The
-        library reads `pts` on its build thread: do not modify the array until that commit returns."""
+        library copies `pts` before this call returns: the caller may reuse the array at once."""
         a = self._cloud(pts)
         p = params or default_params(a.shape[1])
         check(self._lib.gicp_stage_target(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p)), self._ctx,
               "gicp_stage_target")
-        self._staged.append((a, p))
+        self._staged.append((a.shape, p))
 
     def commit_target(self, shard=0, nshards=1):
         """Wait for the oldest staged target; the current target becomes the source, the staged one the target."""
@@ -191,7 +211,7 @@ class Engine:
         if self.n_tgt:
             self.n_src = self.n_tgt
             self.generation += 1
-        self.n_tgt, self.dim = staged[0].shape
+        self.n_tgt, self.dim = staged[0]
 
     def cancel_stage(self):
         """Wait for and drop every staged target."""
@@ -239,12 +259,14 @@ class Engine:
         t[t < 0] = np.nan
         return t
 
-    def set_allreduce(self, fn):
-        """Host statistics exchange (gicp_set_allreduce): fn(buf) gets this rank's statistics as a
-        float64 array and must return (or write in place) the sum over ranks.  None removes it."""
+    def set_allreduce(self, fn, nranks=1, rank=0):
+        """Host statistics exchange (gicp_set_allreduce_ranks): fn(buf) gets this rank's statistics as a
+        float64 array and must return (or write in place) the sum over ranks; (nranks, rank) is what
+        comm_ranks() then reports.  None removes it."""
         if fn is None:
             check(self._lib.gicp_set_allreduce(self._ctx, None, None), self._ctx, "gicp_set_allreduce")
             self._hook = None
+            self._hook_fn = None
             return
 
         def _cb(buf, n, _user):
@@ -260,8 +282,10 @@ class Engine:
                 return -1
 
         cb = _lib.ALLREDUCE_FN(_cb)
-        check(self._lib.gicp_set_allreduce(self._ctx, C.cast(cb, C.c_void_p), None), self._ctx, "gicp_set_allreduce")
+        check(self._lib.gicp_set_allreduce_ranks(self._ctx, C.cast(cb, C.c_void_p), None, int(nranks), int(rank)),
+              self._ctx, "gicp_set_allreduce")
         self._hook = cb
+        self._hook_fn = (fn, int(nranks), int(rank))
 
     def neighbor_counts(self, which="target"):
         w = 0 if which == "target" else 1
@@ -650,9 +674,10 @@ def _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, ta
     G = len(engines)
     k = 5 if full_output else 0
     xchg = _ThreadSum(G) if G > 1 else None
+    prev = [e._hook_fn for e in engines]   # a hook the caller installed on the cached engines
     if xchg is not None:
         for r, e in enumerate(engines):
-            e.set_allreduce(lambda buf, r=r: xchg(r, buf))
+            e.set_allreduce(lambda buf, r=r: xchg(r, buf), nranks=G, rank=r)
 
     def run(r, e):
         try:
@@ -665,9 +690,9 @@ def _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, ta
     try:
         outs = _run_ranks(engines, run)
     finally:
-        if xchg is not None:
-            for e in engines:
-                e.set_allreduce(None)
+        if xchg is not None:   # restore what was there before this call
+            for e, h in zip(engines, prev):
+                e.set_allreduce(*h) if h is not None else e.set_allreduce(None)
     T_fin, res, tr = outs[0]
     iters = int(res["iterations"])
     poses = tr["poses"]

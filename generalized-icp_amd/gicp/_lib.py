@@ -21,6 +21,8 @@ GICP_E_STATE = -3
 GICP_E_COMM = -4
 GICP_E_NOMEM = -5
 COMM_ID_BYTES = 128
+PEER_HANDLE_BYTES = 64
+MAX_PEERS = 16
 PASS_INFO = 6
 GRAPH_K = 20
 
@@ -131,6 +133,11 @@ SIGNATURES = {
     "gicp_get_graph": (C.c_int, [_VP, C.POINTER(C.c_int64), _DP]),
     "gicp_iteration_times": (C.c_int, [_VP, C.POINTER(C.c_float), C.c_int]),
     "gicp_set_allreduce": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),
+    "gicp_set_allreduce_ranks": (C.c_int, [_VP, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    "gicp_peer_export": (C.c_int, [_VP, C.c_char_p]),
+    "gicp_peer_init": (C.c_int, [_VP, C.c_int, C.c_int, C.c_char_p, C.c_double]),
+    "gicp_peer_close": (C.c_int, [_VP]),
+    "gicp_build_info": (C.c_char_p, []),
     "gicp_rotated_covariances": (C.c_int, [_VP, C.c_int, _DP, _DP]),
 }
 
@@ -138,6 +145,28 @@ SIGNATURES = {
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _DP, C.c_int, C.c_void_p)
 
 _lib = None
+
+# the sources gicp_build_info()'s hash covers, in the Makefile's HASH_SRCS order
+HASH_SRCS = ("csrc/gicp_kernels.hip", "csrc/gicp_capi.cpp", "csrc/gicp_solver.cpp", "csrc/gicp_internal.h",
+             "csrc/gicp_solver.h", "csrc/gicp_solve_dev.h", "../include/gicp_hip.h")
+
+
+def source_hash():
+    """First 16 hex digits of sha256 over the library's sources as they lie in this tree (the same
+    bytes the Makefile hashes into gicp_build_info())."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.dirname(HERE)
+    for f in HASH_SRCS:
+        with open(os.path.normpath(os.path.join(pkg, f)), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info():
+    """gicp_build_info() of the loaded library as a dict (src, git, built, arch)."""
+    raw = load().gicp_build_info().decode()
+    return dict(kv.split("=", 1) for kv in raw.split(";") if "=" in kv)
 
 
 def load():

@@ -18,7 +18,7 @@ import numpy as np
 
 from . import Engine, solve_pose
 
-__all__ = ["init_comm", "shard_tiles", "align", "outer_loop"]
+__all__ = ["init_comm", "init_peer", "shard_tiles", "align", "outer_loop"]
 
 
 def init_comm(engine: Engine, rank: int, world: int, group=None):
@@ -29,6 +29,37 @@ def init_comm(engine: Engine, rank: int, world: int, group=None):
     uid = [Engine.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0, group=group)
     engine.comm_init(world, rank, uid[0])
+
+
+def init_peer(engine: Engine, rank: int, world: int, group=None, timeout=10.0):
+    """The in-kernel peer exchange (gicp_peer_export / gicp_peer_init): every rank exports its exchange
+    area, torch.distributed all-gathers the handles, every rank maps its peers' areas and runs the probe
+    exchange.  The outcome is agreed over the group: returns None when every rank has the peer exchange
+    on, else the first failure message seen on any rank (and every rank has closed it, so the caller can
+    fall back to init_comm on all ranks alike)."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    err = None
+    try:
+        h = engine.peer_export()
+    except Exception as e:   # noqa: BLE001 -- reported, and agreed below
+        h, err = b"", f"rank {rank}: {e}"
+    handles = [None] * world
+    dist.all_gather_object(handles, h, group=group)
+    if err is None and all(len(x) == len(h) for x in handles):
+        try:
+            engine.peer_init(world, rank, handles, timeout=timeout)
+        except Exception as e:   # noqa: BLE001
+            err = f"rank {rank}: {e}"
+    elif err is None:
+        err = "a rank could not export its exchange area"
+    errs = [None] * world
+    dist.all_gather_object(errs, err, group=group)
+    first = next((e for e in errs if e is not None), None)
+    if first is not None:
+        engine.peer_close()
+    return first
 
 
 UNIT_TILES = 4      # source tiles per k_corr workgroup (kCorrWaves)

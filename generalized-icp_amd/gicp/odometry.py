@@ -7,8 +7,8 @@ only the new scan is uploaded, sorted, tiled and given covariances.  Given the c
 (`step(scan, next_scan)` / `run(scans, depth)`), their builds run on their own streams from host
 threads while the current pair is registered (`gicp_stage_target` / `gicp_commit_target`, up to
 GICP_MAX_STAGED ahead), so setup leaves the critical path (the demo likewise prepares the next scan
-while its worker registers, robot-visualization.py:239-252).  A staged scan is read by the library's
-build thread: the caller must not modify a scan array until the step that registers it returns.  `gicp(prev, cur)` maps the
+while its worker registers, robot-visualization.py:239-252).  A staged scan is copied by the library
+before stage_target returns, so the caller may refill its buffer at once.  `gicp(prev, cur)` maps the
 previous sensor frame into the current one (p_cur = T p_prev), so the sensor pose advances by
 T^-1: `composition='se3'` (default) is that exact SE(d) update; `composition='reference'` is the
 demo's first-order update (robot-visualization.py:257-265: translation -T[:2, d], yaw
@@ -55,12 +55,14 @@ class Odometry:
         """Add one scan; returns (T, result) of its registration against the previous scan, or
         (None, None) for the first frame.  `next_scan` (or the list `next_scans`, at most
         Engine.MAX_STAGED), if given, is built on the device while this pair is registered; pass the
-        same objects as `scan` of the next calls, in order.  Scans must not be modified until the
-        step that registers them returns (the library reads them on its build threads)."""
+        same objects as `scan` of the next calls, in order (the library copies a staged scan before
+        the call returns: the caller may reuse the array)."""
         t0 = time.perf_counter()
         if self._staged and self._staged[0] is scan:
-            self.eng.commit_target()            # built during an earlier registration
-            self._staged.pop(0)
+            try:
+                self.eng.commit_target()        # built during an earlier registration
+            finally:                            # the library consumed the slot even if its build failed
+                self._staged.pop(0)
         else:
             if self._staged:
                 self.eng.cancel_stage()
@@ -69,13 +71,14 @@ class Odometry:
                 self.eng.target_to_source()
             self.eng.set_target(self._prep(scan), self.params)
         coming = list(next_scans) if next_scan is None else [next_scan, *next_scans]
-        for k, s in enumerate(coming[:self.eng.MAX_STAGED]):
-            if k < len(self._staged):
-                if self._staged[k] is not s:    # a different stream than staged: start over
-                    self.eng.cancel_stage()
-                    self._staged = []
-                else:
-                    continue
+        want = coming[:self.eng.MAX_STAGED]
+        n_ok = 0                                # staged builds that are a prefix of the coming scans
+        while n_ok < min(len(want), len(self._staged)) and self._staged[n_ok] is want[n_ok]:
+            n_ok += 1
+        if n_ok < min(len(want), len(self._staged)):   # a different stream than staged: start over, all of it
+            self.eng.cancel_stage()
+            self._staged = []
+        for s in want[len(self._staged):]:
             self.eng.stage_target(self._prep(s), self.params)
             self._staged.append(s)
         t1 = time.perf_counter()

@@ -136,9 +136,34 @@ int gicp_comm_unique_id(char out[GICP_COMM_ID_BYTES]);   /* rank 0, then broadca
 int gicp_comm_init(gicp_ctx* ctx, int nranks, int rank, const char id[GICP_COMM_ID_BYTES]);
 /* The exchange this context's statistics go through, read back from the communicator itself
  * (ncclCommCount / ncclCommUserRank): *nranks = 1 and *rank = 0 without one; with a host hook
- * (gicp_set_allreduce) the values gicp_comm_init was last given, else 1 / 0.  *kind: 0 none,
- * 1 RCCL, 2 host hook.  Any output may be NULL. */
+ * (gicp_set_allreduce_ranks) the values it was given, else 1 / 0; with the peer exchange
+ * (gicp_peer_init) its nranks / rank.  *kind: 0 none, 1 RCCL, 2 host hook, 3 peer exchange.  Any
+ * output may be NULL. */
 int gicp_comm_ranks(gicp_ctx* ctx, int* nranks, int* rank, int* kind);
+
+/* In-kernel peer exchange (replaces the collective on the per-iteration path).  Every rank
+ * exports one small exchange area of its own device memory (fine-grained, uncached) as an IPC handle
+ * (gicp_peer_export), the handles are all-gathered out of band, and gicp_peer_init maps the peers' areas.
+ * From then on the final workgroup of each correspondence launch writes this rank's statistics into its
+ * slot of every rank's area, raises a per-launch sequence number there, waits (bounded by `timeout_s`)
+ * until every rank's slot of this launch has arrived in its own area, sums them in rank order -- the same
+ * bits on every rank -- and runs the pose solve in the same launch: no collective and no second kernel per
+ * iteration.  gicp_peer_init is collective (every rank, same order of calls) and proves the path with one
+ * probe exchange before it returns; on GICP_E_COMM the context keeps its previous exchange (RCCL / hook /
+ * none).  A timed-out exchange inside gicp_align fails the call with GICP_E_COMM.  `handles` holds
+ * nranks x GICP_PEER_HANDLE_BYTES bytes in rank order (this rank's entry is not opened).  Ranks of one GPU
+ * (several processes) and of several GPUs (xGMI) use the same protocol.  gicp_comm_ranks reports kind 3. */
+#define GICP_PEER_HANDLE_BYTES 64
+#define GICP_MAX_PEERS 16
+int gicp_peer_export(gicp_ctx* ctx, char handle[GICP_PEER_HANDLE_BYTES]);
+int gicp_peer_init(gicp_ctx* ctx, int nranks, int rank, const char* handles, double timeout_s);
+int gicp_peer_close(gicp_ctx* ctx);   /* back to no exchange (RCCL / hook as set before are dropped by init) */
+
+/* Build provenance of this library: "src=<first 16 hex of sha256 over the sources>;git=<rev>;built=<date
+ * time>;arch=gfx950".  The source hash covers csrc/{gicp_kernels.hip, gicp_capi.cpp, gicp_solver.cpp,
+ * gicp_internal.h, gicp_solver.h, gicp_solve_dev.h} and include/gicp_hip.h, concatenated in that order, so
+ * a caller can prove the loaded library was compiled from the sources beside it. */
+const char* gicp_build_info(void);
 
 /* ---- clouds -------------------------------------------------------------- */
 /* Target cloud (gicp.py:101,104): builds the tile index and the per-point
@@ -159,7 +184,8 @@ int gicp_target_to_source(gicp_ctx* ctx, int shard, int nshards);
  * targets -- pinned copy, upload, Morton sort, tiling, covariances, neighbour graph -- each on its own
  * stream from a host thread while the current target is registered (gicp_align on the library's stream
  * runs concurrently).  Up to GICP_MAX_STAGED builds may be pending; commits take them in staging
- * order.  `xyz` must stay valid, and unmodified, until the gicp_commit_target that takes it returns.
+ * order.  `xyz` is copied into a pinned buffer of the slot before gicp_stage_target returns: the caller may
+ * reuse or refill it at once.
  * gicp_commit_target waits for the oldest build, then promotes: current target -> source (as
  * gicp_target_to_source), staged cloud -> target.  gicp_cancel_stage waits for and drops them all. */
 #define GICP_MAX_STAGED 2
@@ -253,6 +279,9 @@ int gicp_iteration_times(gicp_ctx* ctx, float* out, int n);
  * fn = NULL removes the hook. */
 typedef int (*gicp_allreduce_fn)(double* buf, int n, void* user);
 int gicp_set_allreduce(gicp_ctx* ctx, gicp_allreduce_fn fn, void* user);
+/* gicp_set_allreduce that also records the job's (nranks, rank), which gicp_comm_ranks then reports
+ * for the hook (e.g. the device threads of one gicp(devices=[...]) call). */
+int gicp_set_allreduce_ranks(gicp_ctx* ctx, gicp_allreduce_fn fn, void* user, int nranks, int rank);
 
 /* The source covariances rotated by R (dim x dim, row-major): R C_s R^T = a I - (R m)(R m)^T per
  * point, computed on the device (gicp.py:120-121 all_source_cov_matrices, rotated instead of

@@ -36,6 +36,7 @@ class _Ctx:
         self.ptgt = self.psrc = None
         self.shard, self.nshards = 0, 1
         self.hook = None
+        self.hook_ranks = (1, 0)
         self.staged = []          # (points, params) in staging order
         self.last_info = np.zeros(PASS_INFO)
         self.top = None           # (src, tgt, det) of the last pass with want_top_weights
@@ -124,10 +125,13 @@ class FakeLib:
         c = self._c(ctx)
         if not c.staged:
             return self._fail(c, E_STATE, "no staged target")
+        nxt = c.staged.pop(0)      # the slot is consumed even when its build failed (as the library does)
+        if nxt is None:            # a test marked this build as failed
+            return self._fail(c, E_INVALID, "staged build: injected failure")
         if c.tgt is not None:
             c.src = c.tgt
             c.psrc = c.src["p"]
-        c.tgt = c.staged.pop(0)
+        c.tgt = nxt
         c.shard, c.nshards = shard, nshards
         return OK
 
@@ -152,14 +156,19 @@ class FakeLib:
 
     def gicp_comm_ranks(self, ctx, n, r, k):
         c = self._c(ctx)
-        for ptr, v in ((n, c.nshards if c.hook else 1), (r, c.shard if c.hook else 0), (k, 2 if c.hook else 0)):
+        for ptr, v in ((n, c.hook_ranks[0] if c.hook else 1), (r, c.hook_ranks[1] if c.hook else 0),
+                       (k, 2 if c.hook else 0)):
             if ptr:
                 ptr._obj.value = v
         return OK
 
     def gicp_set_allreduce(self, ctx, fn, user):
+        return self.gicp_set_allreduce_ranks(ctx, fn, user, 1, 0)
+
+    def gicp_set_allreduce_ranks(self, ctx, fn, user, nranks, rank):
         c = self._c(ctx)
         c.hook = None if not fn else C.cast(fn, C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p))
+        c.hook_ranks = (nranks, rank) if fn else (1, 0)
         return OK
 
     def gicp_pass_info(self, ctx, out):

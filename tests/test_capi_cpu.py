@@ -32,6 +32,14 @@ def test_library_exports_every_declared_symbol():
     assert set(syms) == set(_lib.SIGNATURES), "ctypes table out of sync with include/gicp_hip.h"
 
 
+def test_build_info_matches_the_sources_in_this_tree():
+    """gicp_build_info() carries the hash of the sources it was compiled from; it must be the hash of
+    the sources beside it (a stale or foreign library fails here)."""
+    info = _lib.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["src"] == _lib.source_hash(), (info, "rebuild: make -C generalized-icp_amd/csrc")
+
+
 def test_basic_host_entry_points():
     lib = _lib.load()
     assert lib.gicp_version() >= 100

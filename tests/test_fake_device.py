@@ -101,3 +101,67 @@ def test_commit_without_stage_is_an_error(fake):
     eng = gicp.Engine(0)
     with pytest.raises(_lib.GicpError):
         eng.commit_target()
+
+
+def test_devices_hook_reports_ranks_and_restores_callers_hook(fake, scene):
+    """gicp(devices=[0, 1]) installs its thread-barrier hook with (nranks, rank) = (2, r), so comm_ranks
+    reports the job while it runs, and puts back the hook a caller had on the cached engines after."""
+    src, tgt, _ = scene
+    kw = dict(max_iterations=3, tolerance=0.0, verbose=False, **P3)
+    eng0 = gicp._engine(0)
+    mine = lambda buf: buf   # noqa: E731 -- an identity hook of the caller's
+    eng0.set_allreduce(mine, nranks=1, rank=0)
+    seen = {}
+    real_align = gicp.Engine.align
+
+    def spy(self, *a, **k):
+        seen[self.device] = self.comm_ranks()
+        return real_align(self, *a, **k)
+
+    import unittest.mock as um
+    with um.patch.object(gicp.Engine, "align", spy):
+        gicp.gicp(src, tgt, devices=[0, 1], **kw)
+    assert seen == {0: (2, 0, "hook"), 1: (2, 1, "hook")}
+    assert eng0._hook_fn[0] is mine and eng0.comm_ranks() == (1, 0, "hook")
+    assert gicp._engine(1).comm_ranks() == (1, 0, "none")
+
+
+def test_odometry_failed_staged_build_then_retry(fake):
+    """A staged build that fails: the step raises, its ring slot is consumed on both sides (the wrapper's
+    list stays in step with the library's), and retrying the same scan registers it correctly (the
+    synchronous path) instead of promoting the next slot's build."""
+    from gicp.odometry import Odometry
+    frames = [f for f, _ in S.lidar_stream(4, beams=8, azimuths=200)]
+    params = gicp.default_params(3, max_iterations=10, tolerance=1e-9, **P3)
+    ref = Odometry(3, params=params)
+    Tref = [ref.step(f)[0] for f in frames]
+    odo = Odometry(3, params=params)
+    odo.step(frames[0], next_scans=frames[1:3])
+    assert odo._staged == [frames[1], frames[2]] or [id(x) for x in odo._staged] == [id(frames[1]), id(frames[2])]
+    fake._c(odo.eng._ctx).staged[0] = None          # frames[1]'s build fails
+    with pytest.raises(ValueError, match="injected"):
+        odo.step(frames[1], next_scans=frames[2:4])
+    assert len(odo._staged) == 1 and odo._staged[0] is frames[2]
+    T1, _ = odo.step(frames[1], next_scans=frames[2:4])   # the retry: built synchronously
+    np.testing.assert_array_equal(T1, Tref[1])
+    T2, _ = odo.step(frames[2])
+    np.testing.assert_array_equal(T2, Tref[2])
+
+
+def test_odometry_restages_whole_lookahead_on_mismatch(fake):
+    """When the coming scans differ from what is staged, every staged build is dropped and the whole
+    look-ahead is staged again (a valid head is not lost); a staged list longer than the look-ahead with
+    a matching prefix is kept."""
+    from gicp.odometry import Odometry
+    frames = [f for f, _ in S.lidar_stream(5, beams=8, azimuths=200)]
+    odo = Odometry(3, params=gicp.default_params(3, max_iterations=5, tolerance=1e-9, **P3))
+    odo.step(frames[0], next_scans=[frames[1], frames[2]])
+    odo.step(frames[1], next_scans=[frames[2], frames[4]])     # head frames[2] still staged: frames[4] added
+    assert [x is y for x, y in zip(odo._staged, [frames[2], frames[4]])] == [True, True]
+    odo.step(frames[2], next_scans=[frames[3], frames[4]])     # staged [4] != coming [3, 4]: restage both
+    assert len(odo._staged) == 2 and odo._staged[0] is frames[3] and odo._staged[1] is frames[4]
+    assert len(fake._c(odo.eng._ctx).staged) == 2
+    odo.step(frames[3], next_scans=[])                        # shorter look-ahead: the staged [4] is kept
+    assert len(odo._staged) == 1 and odo._staged[0] is frames[4]
+    odo.step(frames[4])
+    assert not odo._staged

@@ -310,3 +310,16 @@ def test_reset_cache_changes_no_result(eng, scene3d):
         assert len(t) == 16 and np.sum(~np.isnan(t)) == 2
         times[~np.isnan(t)] = t[~np.isnan(t)]
     assert np.all(times > 0)
+
+
+def test_native_library_built_from_these_sources(eng):
+    """Build provenance on the GPU box: the library this process runs was compiled
+    from exactly the sources in this tree (gicp_build_info's hash = the tree's), and it is the in-tree
+    build (not a copy elsewhere)."""
+    import os
+
+    from gicp import _lib
+    info = _lib.build_info()
+    assert info["src"] == _lib.source_hash(), info
+    assert os.path.dirname(_lib.LIB_PATH) == os.path.dirname(os.path.abspath(gicp.__file__))
+    print(f"gicp_build_info: {info}")

@@ -31,7 +31,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, d, iters, fixed):
+def _rank(rank, world, port, d, iters, fixed, exchange="hook"):
     import torch
     import torch.distributed as dist
 
@@ -48,7 +48,13 @@ def _rank(rank, world, port, d, iters, fixed):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.numpy()
 
-    eng.set_allreduce(allreduce)
+    if exchange == "hook":
+        eng.set_allreduce(allreduce, nranks=world, rank=rank)
+    else:   # the in-kernel peer exchange over IPC-mapped areas (gicp_peer_export / gicp_peer_init)
+        from gicp import distributed as gd
+        err = gd.init_peer(eng, rank, world, timeout=20.0)
+        assert err is None, err
+    kind = eng.comm_ranks()
     eng.set_target(tgt, p)
     eng.set_source(src, p, shard=rank, nshards=world)
     # one pass through gicp_iterate: the exchanged statistics are the full sums
@@ -58,18 +64,20 @@ def _rank(rank, world, port, d, iters, fixed):
     p.tolerance = 1e-9
     T, res = eng.align(None, p)
     np.savez(os.path.join(d, f"rank{rank}.npz"), T=T, st=st, iters=res["iterations"], loss=res["final_loss"],
-             calls=calls[0], corr=res["correspondences"])
+             calls=calls[0], corr=res["correspondences"], kind=np.array(kind, dtype=object), allow_pickle=True)
     eng.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(tmp_path, n, iters, fixed):
+def _run(tmp_path, n, iters, fixed, exchange="hook"):
     src, tgt, Tgt = S.scene_pair_3d(n)
     np.save(tmp_path / "src.npy", src)
     np.save(tmp_path / "tgt.npy", tgt)
-    mp.spawn(_rank, args=(2, _free_port(), str(tmp_path), iters, fixed), nprocs=2, join=True)
-    r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(2)]
+    mp.spawn(_rank, args=(2, _free_port(), str(tmp_path), iters, fixed, exchange), nprocs=2, join=True)
+    r = [dict(np.load(tmp_path / f"rank{k}.npz", allow_pickle=True)) for k in range(2)]
+    for k in range(2):   # what each rank's context reported for its exchange
+        assert tuple(r[k]["kind"]) == (2, k, exchange), r[k]["kind"]
     eng = gicp.Engine(0)
     try:
         p = gicp.default_params(3, **P3)
@@ -85,13 +93,17 @@ def _run(tmp_path, n, iters, fixed):
     return r, st1, T1, res1, Tgt
 
 
-def test_two_ranks_one_gpu_1m_30_iterations(tmp_path):
-    """C4's protocol at full size: 1M/1M, 30 fixed iterations, two source shards."""
-    r, st1, T1, res1, Tgt = _run(tmp_path, 1_000_000, 30, fixed=True)
+@pytest.mark.parametrize("exchange", ["hook", "peer"])
+def test_two_ranks_one_gpu_1m_30_iterations(tmp_path, exchange):
+    """C4's protocol at full size: 1M/1M, 30 fixed iterations, two source shards; the statistics meet
+    through the host hook (gloo) or in-kernel through the IPC-mapped peer areas (the solve then runs in
+    each rank's k_corr launch)."""
+    r, st1, T1, res1, Tgt = _run(tmp_path, 1_000_000, 30, fixed=True, exchange=exchange)
     assert np.array_equal(r[0]["T"], r[1]["T"]), "ranks disagree: the exchanged sums must give identical solves"
     assert np.array_equal(r[0]["st"], r[1]["st"])
     assert int(r[0]["iters"]) == int(r[1]["iters"]) == 30
-    assert int(r[0]["calls"]) == 31   # one exchange per pass: the gicp_iterate pass + 30 in align
+    # one exchange per pass: the gicp_iterate pass + 30 in align (host hook), none through the host (peer)
+    assert int(r[0]["calls"]) == (31 if exchange == "hook" else 0)
     # the sum over the two shards = the one-process pass (summation order differs: fp64 rounding)
     scale = np.maximum(np.abs(st1), 1e-12 * np.abs(st1).max())
     assert np.max(np.abs(r[0]["st"] - st1) / scale) < 1e-9
@@ -100,10 +112,67 @@ def test_two_ranks_one_gpu_1m_30_iterations(tmp_path):
     assert S.rotation_angle_error(T1, Tgt) < 1e-4 and S.translation_error(T1, Tgt) < 1e-3
 
 
-def test_two_ranks_converge_on_the_same_iteration(tmp_path):
+@pytest.mark.parametrize("exchange", ["hook", "peer"])
+def test_two_ranks_converge_on_the_same_iteration(tmp_path, exchange):
     """Convergence on (gicp.py:155-162): both ranks stop at the same iteration as one process."""
-    r, _, T1, res1, _ = _run(tmp_path, 20_000, 60, fixed=False)
+    r, _, T1, res1, _ = _run(tmp_path, 20_000, 60, fixed=False, exchange=exchange)
     assert np.array_equal(r[0]["T"], r[1]["T"])
     assert int(r[0]["iters"]) == int(r[1]["iters"])
     assert abs(int(r[0]["iters"]) - int(res1["iterations"])) <= 1
     np.testing.assert_allclose(r[0]["T"], T1, rtol=0, atol=1e-8)
+
+
+def _rank_timeout(rank, world, port, d):
+    """Rank 1 stops early: rank 0's next exchange must time out inside the kernel (bounded wait), fail
+    its call with GICP_E_COMM, and leave the context usable."""
+    import torch.distributed as dist
+    from gicp import _lib
+    from gicp import distributed as gd
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src, tgt = np.load(os.path.join(d, "src.npy")), np.load(os.path.join(d, "tgt.npy"))
+    p = gicp.default_params(3, fixed_iterations=1, **P3)
+    eng = gicp.Engine(0)
+    out = {}
+    assert gd.init_peer(eng, rank, world, timeout=0.5) is None
+    eng.set_target(tgt, p)
+    eng.set_source(src, p, shard=rank, nshards=world)
+    p.max_iterations = 4 if rank == 0 else 2
+    try:
+        eng.align(None, p)
+        out["err"] = 0
+    except _lib.GicpError as e:
+        out["err"] = e.code
+    dist.barrier()
+    # the second peer_init probe: rank 1 never joins, so rank 0's probe times out
+    if rank == 0:
+        eng.peer_close()
+        h = eng.peer_export()
+        try:
+            eng.peer_init(2, 0, [h, h], timeout=0.5)   # rank 1's slot: its own handle is not opened
+            out["probe"] = 0
+        except _lib.GicpError as e:
+            out["probe"] = e.code
+        out["kind"] = eng.comm_ranks()[2]
+        p.max_iterations = 3   # alone again: the context still registers
+        T, res = eng.align(None, p)
+        out["after"] = int(res["iterations"])
+    np.save(os.path.join(d, f"to{rank}.npy"), np.array(out, dtype=object), allow_pickle=True)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_peer_exchange_times_out_instead_of_hanging(tmp_path):
+    src, tgt, _ = S.scene_pair_3d(20_000)
+    np.save(tmp_path / "src.npy", src)
+    np.save(tmp_path / "tgt.npy", tgt)
+    mp.spawn(_rank_timeout, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = np.load(tmp_path / "to0.npy", allow_pickle=True).item()
+    r1 = np.load(tmp_path / "to1.npy", allow_pickle=True).item()
+    from gicp import _lib
+    assert r1["err"] == 0                       # the rank that stopped first finished its 2 iterations
+    assert r0["err"] == _lib.GICP_E_COMM        # its peer's third exchange never came: bounded, reported
+    assert r0["probe"] == _lib.GICP_E_COMM and r0["kind"] == "none"
+    assert r0["after"] == 3

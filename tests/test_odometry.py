@@ -177,3 +177,30 @@ def test_stage_ring_limits_and_order():
         assert np.all(np.isfinite(T))
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_staged_scan_buffer_may_be_refilled_at_once():
+    """gicp_stage_target copies the caller's scan before it returns, so a sensor
+    buffer refilled right after staging still registers the scan it held -- bit-identical to building
+    that scan synchronously."""
+    import gicp
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    f = [s for s, _ in S.lidar_stream(2)]
+    p = gicp.default_params(3, max_iterations=20, tolerance=1e-9, **kw)
+    a, b = gicp.Engine(0), gicp.Engine(0)
+    try:
+        a.set_target(f[0], p)
+        buf = np.ascontiguousarray(f[1].copy())
+        a.stage_target(buf, p)
+        buf[:] = buf[::-1] + 7.0            # the sensor overwrites its buffer at once
+        a.commit_target()
+        Ta, ra = a.align(None, p)
+        b.set_target(f[0], p)
+        b.target_to_source()
+        b.set_target(f[1], p)
+        Tb, rb = b.align(None, p)
+    finally:
+        a.close()
+        b.close()
+    assert np.array_equal(Ta, Tb) and ra["iterations"] == rb["iterations"]
