@@ -137,19 +137,27 @@ def workload(n, dim):
         f"2d_segments_{n // 1000}k_k6"
 
 
-def measured_traffic(workload):
-    """HBM-side bytes per k_corr launch from the newest committed PMC summary of this workload
-    (scripts/profile_round.sh -> profiles/rNN/pmc_traffic.json); the counters cannot be read
-    in-process, so bench.py reports the profiled value of the same command and names its file."""
+def measured_traffic(workload, steps, warmup):
+    """HBM-side bytes per k_corr launch from the newest committed PMC summary of THIS command -- the same
+    workload, --steps and --warmup (scripts/profile_round.sh -> profiles/rNN/pmc_traffic.json); the counters
+    cannot be read in-process.  Returns (bytes, file, per_pass, note); bytes is None, with the reason in
+    note, when no profile of this exact command exists (another command's bytes are never reported)."""
     import glob
+    seen = []
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload:
-            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT), d.get("per_pass")
-    return None, None, None
+        if d.get("workload") != workload:
+            continue
+        key = (d.get("steps"), d.get("warmup"))
+        if key == (steps, warmup):
+            return d["traffic_bytes_per_launch"], os.path.relpath(f, ROOT), d.get("per_pass"), \
+                f"profiled: rocprofv3 --pmc of bench.py --gpus 1 --steps {steps} --warmup {warmup} ({d.get('launches')} launches)"
+        seen.append(f"{os.path.relpath(f, ROOT)} (steps {key[0]}, warmup {key[1]})")
+    return None, None, None, ("no PMC profile of this command (steps %d, warmup %d)%s" %
+                              (steps, warmup, ("; other commands' profiles not used: " + ", ".join(seen)) if seen else ""))
 
 
 def cpu_baseline(src, tgt, kw, workers, iters=1):
@@ -300,7 +308,9 @@ def main():
     achieved = alg_bytes / (corr_avg_ms * 1e-3) / 1e9
     n_mov = min(10, a.steps)
     pairs = res["pairs_total"] / a.steps / world   # mean per launch (summed over ranks by the all-reduce)
-    traffic, traffic_src, traffic_pp = measured_traffic(name) if world == 1 else (None, None, None)
+    traffic, traffic_src, traffic_pp, traffic_note = (measured_traffic(name, a.steps, a.warmup) if world == 1 and
+                                                      a.shard_sim <= 1 and not a.warm else
+                                                      (None, None, None, "not profiled (multi-rank or diagnostic run)"))
     line = {
         "metric": "GICP iterations/sec (and ms/iter) at N points, 1/2/4/8 GPU; final transform error",
         "value": a.steps / elapsed,
@@ -326,6 +336,7 @@ def main():
         "comm_fallback": peer_note,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_note": traffic_note,
                      "traffic_per_pass": None if not traffic_pp else
                      {k: traffic_pp.get(k) for k in ("first_pass", "moving_mean", "converged_mean", "timed_mean")},
                      "traffic_vs_alg": None if not traffic_pp else

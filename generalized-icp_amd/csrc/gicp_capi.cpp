@@ -1055,6 +1055,7 @@ void close_peers(gicp_ctx* c) {
 int guard_impl(gicp_ctx* c, const char* where, const std::function<void()>& body) {
     try {
         if (c) HIPCHK(hipSetDevice(c->device));
+        (void)hipGetLastError();   // a failure an earlier call reported must not fail this call's first launch
         body();
         return GICP_OK;
     } catch (const Fail& f) {
@@ -1730,9 +1731,11 @@ int gicp_peer_init(gicp_ctx* c, int nranks, int rank, const char* handles, doubl
                 std::memcpy(&h, handles + (size_t)r * GICP_PEER_HANDLE_BYTES, sizeof(h));
                 void* ptr = nullptr;
                 const hipError_t e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
-                if (e != hipSuccess)
+                if (e != hipSuccess) {
+                    (void)hipGetLastError();
                     throw Fail{GICP_E_COMM, std::string("hipIpcOpenMemHandle(rank ") + std::to_string(r) + "): " +
                                                 hipGetErrorString(e)};
+                }
                 c->peer_open[r] = ptr;
                 area[r] = static_cast<double*>(ptr);
             }

@@ -22,7 +22,7 @@ from . import _lib
 from ._lib import Debug, Params, Result, Trace, check, dptr
 
 __all__ = ["gicp", "apply_transformation", "Engine", "RotatedCovariances", "expand_stats", "stats_size",
-           "default_params"]
+           "default_params", "last_result"]
 
 
 def stats_size(dim):
@@ -436,6 +436,14 @@ def _cg_inner_faithful(src, q, W, offset):
 
 
 _ENGINES = {}
+_LAST_RESULT = None
+
+
+def last_result():
+    """The gicp_result of the last gicp() call that ran its loop on the device (mode='fast',
+    inner='newton'; the first device's): iterations, wall_ms (the library's own wall time of the loop,
+    without the clouds' setup and the 7-tuple's assembly), stop reason, ...  None before such a call."""
+    return None if _LAST_RESULT is None else dict(_LAST_RESULT)
 
 # 2-D clouds up to this size default to mode='faithful' (scipy fmin_cg on the reference's per-point
 # loss, which copies N x 2 x 2 weights to the host every iteration); larger ones to mode='fast'
@@ -694,6 +702,8 @@ def _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, ta
             for e, h in zip(engines, prev):
                 e.set_allreduce(*h) if h is not None else e.set_allreduce(None)
     T_fin, res, tr = outs[0]
+    global _LAST_RESULT
+    _LAST_RESULT = dict(res)
     iters = int(res["iterations"])
     poses = tr["poses"]
     loss_stop = bool(res["converged"]) and res["stop_reason"] == "loss"

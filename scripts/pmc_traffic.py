@@ -4,6 +4,9 @@ corrected as MI355X_MICROARCH.md §HBM prescribes (gfx950 FETCH_SIZE counts half
 
     python scripts/pmc_traffic.py <pmc dir> <out.json> [kernel substring] [workload] [first] [passes]
 
+first = the command's --warmup, passes = its --steps: the summary is keyed by (workload, steps, warmup) and
+bench.py reports it only for that exact command.
+
 Besides the mean over every launch of the command, per pass of the timed registration (dispatches
 [first, first + passes) of the kernel: bench.py's 5 warmup launches come first): pass 0, the mean of
 passes 1-10 (moving) and of the last 10 (converged)."""
@@ -31,7 +34,9 @@ fp, wp = timed("FETCH_SIZE"), timed("WRITE_SIZE")
 per = [(2.0 * a + b) * 1024.0 for a, b in zip(fp, wp)] if len(fp) == len(wp) else []
 fetch = sum(vals["FETCH_SIZE"]) / max(1, len(vals["FETCH_SIZE"]))
 write = sum(vals["WRITE_SIZE"]) / max(1, len(vals["WRITE_SIZE"]))
-res = {"kernel": kern, "workload": workload, "launches": len(vals["FETCH_SIZE"]),
+res = {"kernel": kern, "workload": workload, "steps": passes, "warmup": first,
+       "command": f"bench.py --gpus 1 --steps {passes} --warmup {first}",
+       "launches": len(vals["FETCH_SIZE"]),
        "fetch_size_kib": fetch, "write_size_kib": write,
        "traffic_bytes_per_launch": (2.0 * fetch + write) * 1024.0,
        "per_pass": None if not per else {
