@@ -353,11 +353,13 @@ def main():
                                      "k_corr's final workgroup also runs the one-wave inner solve and pose update "
                                      "(~5 us, inside the timed duration)" +
                                      (", after the in-kernel peer exchange" if comm_kind == "peer" else ""))},
-        "passes": {"moving_pass_us": float(np.mean(per_iter[:n_mov])) * 1e3,
+        "passes": {"moving_pass_us": float(np.mean(per_iter[1:1 + n_mov])) * 1e3,
+                   "passes_0_9_us": float(np.mean(per_iter[:n_mov])) * 1e3,
                    "converged_pass_us": float(np.mean(per_iter[-n_mov:])) * 1e3,
                    "first_pass_us": float(per_iter[0]) * 1e3,
                    "k_corr_us_per_iteration": [round(float(x) * 1e3, 1) for x in per_iter],
-                   "note": "moving = mean k_corr of iterations 1-10 (the pose still moves), converged = last 10"},
+                   "note": "moving = mean k_corr of iterations 1-10 (the pose still moves; rounds 1-3 reported "
+                           "iterations 0-9 under this name, now passes_0_9_us), converged = last 10"},
         "warm_start": None if warm_elapsed is None else
         {"value": a.steps / warm_elapsed, "ms_per_step": warm_elapsed * 1e3 / a.steps,
          "note": "diagnostic, not the metric: the same K iterations again, continuing from the caches"},

@@ -174,7 +174,7 @@ struct Cloud {
     int32_t* nbi = nullptr;           // ... and their sorted indices
     bool graph_ready = false;
     bool cov_ready = false;
-    int cov_q_begin = 0, cov_q_end = 0;  // tiles whose covariances were computed
+    int cov_shard = 0, cov_nshards = 1;  // whose tiles' covariances were computed (build_cloud)
 
     size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
     size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0, cap_boxes = 0, cap_seed = 0;
@@ -550,8 +550,22 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
 
 // Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
 // is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
+// Tiles of shard `shard` of `nshards` (the k_corr split: chunks of kShardChunk units of kCorrWaves tiles, dealt
+// round-robin), or all of them when nshards = 1.
+int shard_tile_count(int ntiles, int shard, int nshards) {
+    if (nshards <= 1) return ntiles;
+    constexpr int kChunkTiles = kShardChunk * kCorrWaves;
+    const int nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    int mine = 0;
+    for (int c = shard; c < nchunks; c += nshards) mine += std::min(kChunkTiles, ntiles - c * kChunkTiles);
+    return mine;
+}
+
+// cov_shard / cov_nshards: the covariances are computed for that shard's tiles only (a sharded source: every
+// rank needs the whole cloud's index for the neighbourhoods, but only its own tiles' covariances); the other
+// rows read NaN.
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
-                 BuildScratch& bs, hipStream_t st, bool staged = false) {
+                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -676,12 +690,15 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         std::memcpy(&cl.rho, &rho_bits, sizeof(float));
         tick("tiles");
 
-        // surface covariances (gicp.py:19-35)
-        const int qb = 0, qe = cl.ntiles;
+        // surface covariances (gicp.py:19-35), of this rank's tiles when sharded
+        const int qb = 0, qe = shard_tile_count(cl.ntiles, cov_shard, cov_nshards);
         CovArgs ca{};
         ca.cl = cl.view();
         ca.q_begin = qb;
         ca.q_end = qe;
+        ca.sh_n = cov_nshards;
+        ca.sh_r = cov_shard;
+        if (cov_nshards > 1) HIPCHK(hipMemsetAsync(cl.cov, 0xFF, sizeof(double4) * n, st));   // NaN: not computed
         const double dn = p.max_distance_nearest_neighbors;
         ca.mg = make_margin(dim, cl.rho, cl.rho, dn);
         ca.search2 = screen_bound(ca.mg, dn);
@@ -727,8 +744,8 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         if (graph) HIPCHK(launch_graph_pack(ga, st));
         HIPCHK(hipStreamSynchronize(st));
         cl.cov_ready = true;
-        cl.cov_q_begin = qb;
-        cl.cov_q_end = qe;
+        cl.cov_shard = cov_shard;
+        cl.cov_nshards = cov_nshards;
         cl.graph_ready = graph;
         tick(graph ? "covariances+graph" : "covariances");
         if (verbose)
@@ -753,6 +770,8 @@ void reset_tile_state(gicp_ctx* c) {
 
 void set_shard(gicp_ctx* c, int shard, int nshards) {
     if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
+    if (c->src.cov_nshards > 1 && (c->src.cov_nshards != nshards || c->src.cov_shard != shard))
+        throw Fail{GICP_E_INVALID, "the source's covariances were computed for another shard"};
     c->shard = shard;
     c->nshards = nshards;
     c->q_begin = 0;   // k_corr maps this rank's units onto the cloud's (interleaved chunks)
@@ -1256,7 +1275,7 @@ int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gi
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         c->psrc = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c->src, xyz, N, dim, c->psrc, false, c->bs, c->stream);
+        build_cloud(c->src, xyz, N, dim, c->psrc, false, c->bs, c->stream, false, shard, nshards);
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
     });

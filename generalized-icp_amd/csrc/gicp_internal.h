@@ -122,7 +122,10 @@ static_assert(8 + 6 * kGraphK <= 128, "a graph row is one 128-B line");
 
 struct CovArgs {
     DevCloud cl;
-    int32_t q_begin, q_end;   // query tiles
+    int32_t q_begin, q_end;   // query tiles, counted within this rank's shard (all tiles when sh_n = 1)
+    // source shards (the k_corr split, gicp_internal.h kShardChunk): this rank's query tile t is the cloud's
+    // tile ((t / 64) sh_n + sh_r) 64 + t % 64 -- a rank computes the covariances of its own tiles only
+    int32_t sh_n, sh_r;
     // waves per query tile: 1 (the tile's 64 points, one per lane), or kSub (one wave per 16-row sub-tile,
     // its box the sub-box: a small cloud -- a 100k stream frame is ~1.7k tiles, a third of one wave per
     // SIMD -- is bound by its longest neighbourhood walk, which the smaller box shortens)

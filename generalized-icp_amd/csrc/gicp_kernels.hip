@@ -863,11 +863,14 @@ __device__ __forceinline__ double4 cov_descriptor(const CovSums<D>& A, int min_n
 // is unchanged); the culling box `qb` is the part's sub-box (centre c + sc, half-extents sh) when split.
 // Returns the tile index, -1 if the wave has no rows.
 template <int D>
-__device__ __forceinline__ int split_query(const DevCloud& cl, int first, int last, int split, TileInfo& qt,
-                                          Query<D>& q, Query<D>& qb, int& i) {
+__device__ __forceinline__ int split_query(const DevCloud& cl, int first, int last, int split, int sh_n, int sh_r,
+                                          TileInfo& qt, Query<D>& q, Query<D>& qb, int& i) {
     const int wid = (int)blockIdx.x * kWavesPerWG + ((int)threadIdx.x >> 6), l = (int)threadIdx.x & 63;
-    const int T = first + wid / split, g = wid % split;
-    if (T >= last) return -1;
+    const int Tl = first + wid / split, g = wid % split;
+    if (Tl >= last) return -1;
+    constexpr int kChunkTiles = kShardChunk * kCorrWaves;   // tiles per shard chunk (k_corr's split)
+    const int T = sh_n > 1 ? ((Tl / kChunkTiles) * sh_n + sh_r) * kChunkTiles + Tl % kChunkTiles : Tl;
+    if (T >= cl.ntiles) return -1;
     qt = tile_meta(cl, T);
     const int rows = kTile / split, r0 = g * rows, r1 = min(qt.count, r0 + rows);
     if (r0 >= r1) return -1;
@@ -909,7 +912,7 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
     TileInfo qt;
     Query<D> q, qb;
     int i = 0;
-    const int T = split_query<D>(cl, A.q_begin, A.q_end, A.split, qt, q, qb, i);
+    const int T = split_query<D>(cl, A.q_begin, A.q_end, A.split, A.sh_n, A.sh_r, qt, q, qb, i);
     if (T < 0) return;  // waves are independent (no workgroup barrier here)
 
     // ---- phase 1: fp32 screen for the K+1 smallest keys ------------------
@@ -1121,7 +1124,8 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 // key_d2(tau) - margin); a lane that found fewer keys within the screen radius has every target within it:
 // r2 = search2 - margin.
 // Pack the graph rows into one 128-B line each (GraphArgs / DevCloud::nbq): offsets quantised to
-// int16 in units of s = max |offset| / 32767 (error <= s / 2 per axis, which k_corr's bound adds).
+// int16 in units of s = max |offset| / 32767 (error <= s / 2 per axis, which k_corr's bound adds),
+// entries ordered nearest-first.
 __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ nb, const float2* __restrict__ nbh,
                                                     int64_t n, uint4* __restrict__ nbq, int32_t* __restrict__ nbi) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1135,6 +1139,23 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
     }
     const float s = m > 0.f ? m / 32767.f : 1e-30f;
     const float inv = 1.f / s;
+    // entries nearest-first (squared offset length, ties by sorted index): k_corr's descent reads a row's
+    // first half and needs the second only when an entry there could still be the nearest
+    float key[kGraphK];
+    int ord[kGraphK];
+    for (int k = 0; k < cnt; ++k) {
+        const float4 v = nb[i * kGraphK + k];
+        const float kk = fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+        const int t = __float_as_int(v.w);
+        int pos = k;
+        while (pos > 0 && (key[pos - 1] > kk || (key[pos - 1] == kk && __float_as_int(nb[i * kGraphK + ord[pos - 1]].w) > t))) {
+            key[pos] = key[pos - 1];
+            ord[pos] = ord[pos - 1];
+            --pos;
+        }
+        key[pos] = kk;
+        ord[pos] = k;
+    }
     uint32_t w[32];
     w[0] = __float_as_uint(h.x);
     w[1] = __float_as_uint(s);
@@ -1147,7 +1168,7 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
     for (int k = 0; k < kGraphK; ++k) {
         int idx = -1;
         if (k < cnt) {
-            const float4 v = nb[i * kGraphK + k];
+            const float4 v = nb[i * kGraphK + ord[k]];
             const float c[3] = {v.x, v.y, v.z};
             for (int a = 0; a < 3; ++a) q[a] = (int16_t)max(-32767, min(32767, __float2int_rn(c[a] * inv)));
             idx = __float_as_int(v.w);
@@ -1213,6 +1234,9 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 
 #ifndef GICP_ROW_SPLIT
 #define GICP_ROW_SPLIT 9
+#endif
+#ifndef GICP_NBI_SPEC
+#define GICP_NBI_SPEC 0
 #endif
 constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
 
@@ -1499,14 +1523,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     load_half(0);
                     const float r = __uint_as_float(w[0]), sc = __uint_as_float(w[1]);
                     const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
-                    float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f;
+                    float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f, rho = 0.f;
                     int bk = -1;
-#pragma unroll
-                    for (int k = 0; k < kGraphK; ++k) {
-                        if (k == kRowSplit) {
-                            asm volatile("" ::: "memory");   // keep the second half's loads here
-                            load_half(4);
-                        }
+                    auto entry = [&](int k) {
                         int c3[3];
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
@@ -1528,11 +1547,39 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         } else {   // (non-negative floats order like their bits: v_min_u32, no NaN canonicalisation)
                             b2 = __uint_as_float(min(__float_as_uint(b2), __float_as_uint(dd)));
                         }
-                    }
+                        if (k == kRowSplit - 1) {   // |offset| of the first half's last entry (quantised)
+                            const float ox = sc * (float)c3[0], oy = sc * (float)c3[1], oz = sc * (float)c3[2];
+                            rho = __builtin_amdgcn_sqrtf(fmaf(ox, ox, fmaf(oy, oy, oz * oz)));
+                        }
+                    };
+#pragma unroll
+                    for (int k = 0; k < kRowSplit; ++k) entry(k);
+#if GICP_NBI_SPEC
+                    // the first half's winner's sorted index, requested now: in flight with the second half,
+                    // and the hop (or the certificate) needs no further round trip when the winner stays
+                    const int bk_half = bk;
+                    int nb_spec = node;
+                    if (bk >= 0) nb_spec = tg.nbi[(int64_t)node * kGraphK + bk];
+                    asm volatile("" ::: "memory");
+#endif
                     const float d0 = __builtin_amdgcn_sqrtf(d0s);
-                    const float e1 = __builtin_amdgcn_sqrtf(b1), e2 = __builtin_amdgcn_sqrtf(b2);
                     // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
                     const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
+                    // The row is sorted nearest-first (k_graph_pack): every entry of the second half lies at
+                    // >= rho - s from the node (quantisation), so at >= rho - s - d0 - e from p' and screens
+                    // >= lc.  It is read only by lanes where such an entry could still be the nearest or
+                    // within the tie band of it; elsewhere lc bounds the runner-up (sound for the gap).
+                    const float lc = rho - sc - d0 - 2.f * e;
+                    const bool need2 = lc <= __builtin_amdgcn_sqrtf(b1) + 2.f * e;
+                    if (wave_any(need2)) {
+                        if (need2) {
+                            load_half(4);
+#pragma unroll
+                            for (int k = kRowSplit; k < kGraphK; ++k) entry(k);
+                        }
+                    }
+                    if (!need2) b2 = fminf(b2, lc * lc);
+                    const float e1 = __builtin_amdgcn_sqrtf(b1), e2 = __builtin_amdgcn_sqrtf(b2);
                     if (e2 - e1 <= 2.f * e) {
                         // near tie: if the row covers it (same test as below), the nearest is one of the
                         // candidates within e1 + 2e, resolved exactly after the loop
@@ -1542,7 +1589,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         act = false;                              // else the walk decides
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
+#if GICP_NBI_SPEC
+                        cj = bk == bk_half ? nb_spec : tg.nbi[(int64_t)node * kGraphK + bk];
+#else
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
+#endif
                         ggap = fminf(e2, r - d0) - e1 - 2.f * e;
                         act = false;
                     } else if (bk < 0) {
@@ -1552,7 +1603,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         qr[1] = by;
                         qr[2] = bz;
                         eq = e;
+#if GICP_NBI_SPEC
+                        node = bk == bk_half ? nb_spec : tg.nbi[(int64_t)node * kGraphK + bk];
+#else
                         node = tg.nbi[(int64_t)node * kGraphK + bk];
+#endif
                     }
                 }
             }

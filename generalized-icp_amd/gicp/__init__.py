@@ -666,6 +666,10 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     eng = engines[0]
     target_cov = eng.covariances("target")
     init_src_cov = eng.covariances("source")
+    for e in engines[1:]:   # each device computed its own shard's source covariances (NaN elsewhere)
+        other = e.covariances("source")
+        miss = np.isnan(init_src_cov[:, 0, 0])
+        init_src_cov[miss] = other[miss]
     T = np.eye(d + 1) if T0 is None else np.array(T0, dtype=np.float64)
     if mode == "fast" and inner == "newton":
         for k, v in pcl.items():

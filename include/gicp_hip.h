@@ -169,11 +169,14 @@ const char* gicp_build_info(void);
 /* Target cloud (gicp.py:101,104): builds the tile index and the per-point
  * surface covariances once; reusable across gicp_align calls. */
 int gicp_set_target(gicp_ctx* ctx, const double* xyz, int64_t M, int dim, const gicp_params* p);
-/* Source cloud (gicp.py:100,111): the whole cloud is uploaded (its
+/* Source cloud (gicp.py:100,111): the whole cloud is uploaded and indexed (its
  * covariance neighbourhoods need every point); this rank reduces only the
  * source tiles of shard `shard` of `nshards`: the cloud's Morton-ordered
  * tiles in chunks of 64, dealt round-robin (chunks shard, shard + nshards, ...;
- * gicp/distributed.py shard_tiles states the same split). */
+ * gicp/distributed.py shard_tiles states the same split), and computes the
+ * covariances of those tiles only (with nshards > 1, gicp_get_covariances /
+ * gicp_rotated_covariances of the source give NaN rows for the other shards'
+ * points: merge them across ranks). */
 int gicp_set_source(gicp_ctx* ctx, const double* xyz, int64_t N, int dim, const gicp_params* p,
                     int shard, int nshards);
 /* Promote the current target (index + covariances) to be the next source,

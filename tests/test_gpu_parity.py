@@ -173,6 +173,27 @@ def test_sharded_statistics_sum_to_full(eng, scene3d):
     np.testing.assert_allclose(np.sum(parts, axis=0), full, rtol=1e-12, atol=1e-12 * np.max(np.abs(full)))
 
 
+def test_sharded_source_computes_its_own_covariances(eng, scene3d):
+    """a sharded source builds the covariances of its own tiles only -- those rows equal
+    the unsharded build's bit for bit, the other rows are NaN, and the shards' rows partition the cloud."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    full = eng.covariances("source")
+    assert not np.isnan(full).any()
+    owner = np.full(len(src), -1)
+    for s in range(3):
+        eng.set_source(src, p, shard=s, nshards=3)
+        c = eng.covariances("source")
+        mine = ~np.isnan(c[:, 0, 0])
+        assert np.isnan(c[~mine]).all() and not np.isnan(c[mine]).any()
+        assert np.array_equal(c[mine], full[mine])
+        assert np.all(owner[mine] == -1)
+        owner[mine] = s
+    assert np.all(owner >= 0)
+
+
 def test_iterate_is_deterministic(eng, scene3d):
     src, tgt, _ = scene3d
     p = gicp.default_params(3, **P3)
@@ -336,6 +357,9 @@ def test_target_graph_rows_cover_their_radius(eng, scene3d):
     for i in range(0, len(tgt), 97):
         row = idx[i][idx[i] >= 0]
         assert i not in row and len(set(row)) == len(row)
+        assert np.all(idx[i][len(row):] < 0)                   # real entries first, then the -1 pads
+        d = np.linalg.norm(tgt[row] - tgt[i], axis=1)          # nearest-first (the descent's early exit)
+        assert np.all(np.diff(d) >= -1e-6 * (1.0 + d[1:])), (i, d)
         ball = [t for t in tree.query_ball_point(tgt[i], rad[i]) if t != i and np.linalg.norm(tgt[t] - tgt[i]) < rad[i]]
         assert set(ball) <= set(row), i
 
