@@ -1235,9 +1235,6 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 #ifndef GICP_ROW_SPLIT
 #define GICP_ROW_SPLIT 9
 #endif
-#ifndef GICP_NBI_SPEC
-#define GICP_NBI_SPEC 0
-#endif
 constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
 
 // In-kernel exchange of a workgroup's NV values with every peer rank (PeerArgs, gicp_internal.h), called by
@@ -1554,14 +1551,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     };
 #pragma unroll
                     for (int k = 0; k < kRowSplit; ++k) entry(k);
-#if GICP_NBI_SPEC
-                    // the first half's winner's sorted index, requested now: in flight with the second half,
-                    // and the hop (or the certificate) needs no further round trip when the winner stays
-                    const int bk_half = bk;
-                    int nb_spec = node;
-                    if (bk >= 0) nb_spec = tg.nbi[(int64_t)node * kGraphK + bk];
-                    asm volatile("" ::: "memory");
-#endif
                     const float d0 = __builtin_amdgcn_sqrtf(d0s);
                     // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
                     const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
@@ -1589,11 +1578,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         act = false;                              // else the walk decides
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
-#if GICP_NBI_SPEC
-                        cj = bk == bk_half ? nb_spec : tg.nbi[(int64_t)node * kGraphK + bk];
-#else
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
-#endif
                         ggap = fminf(e2, r - d0) - e1 - 2.f * e;
                         act = false;
                     } else if (bk < 0) {
@@ -1603,11 +1588,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         qr[1] = by;
                         qr[2] = bz;
                         eq = e;
-#if GICP_NBI_SPEC
-                        node = bk == bk_half ? nb_spec : tg.nbi[(int64_t)node * kGraphK + bk];
-#else
                         node = tg.nbi[(int64_t)node * kGraphK + bk];
-#endif
                     }
                 }
             }
