@@ -637,8 +637,8 @@ __device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, in
 // within the shrinking bound -- 3 round trips before the first visit instead of the hierarchy's ~10, and
 // fewer visits (the bound shrinks fastest nearest-first).  Every tile within the initial reach is a candidate
 // (its centre's cell is in the range), so the walk visits whatever else it needs: the results are identical.
-// The cells are taken 64 per round (one round unless the reach is large against the cells).  The sorted
-// candidates wait in the wave's LDS (the fp64 staging area, free during the walk), not in registers.
+// The cells are taken 64 per round (one round unless the reach is large against the cells).  The candidates'
+// records wait in the wave's LDS (the fp64 staging area, free during the walk), only their keys in registers.
 template <int D, class VisitPre, class WB, class Collect, class Cnt = NoCount>
 __device__ __forceinline__ void walk_g(const DevCloud& db, const Query<D>& q, WaveLds& L, VisitPre&& visit_pre,
                                        WB&& wave_bound, float skin, Collect&& collect, Cnt* cnt = nullptr) {
@@ -666,10 +666,9 @@ __device__ __forceinline__ void walk_g(const DevCloud& db, const Query<D>& q, Wa
         nc[a] = __builtin_amdgcn_readfirstlane(max(0, a1 - a0 + 1));
         ncq *= nc[a];
     }
-    float* const sk = reinterpret_cast<float*>(L.t.x64);          // sorted candidates: gap key,
-    int32_t* const stt = reinterpret_cast<int32_t*>(L.t.x64) + kWave;   // tile,
-    int32_t* const sst = reinterpret_cast<int32_t*>(L.t.y64);     // first point,
-    int32_t* const scn = reinterpret_cast<int32_t*>(L.t.y64) + kWave;   // point count
+    int32_t* const stt = reinterpret_cast<int32_t*>(L.t.x64);             // candidate of lane l: tile,
+    int32_t* const sst = reinterpret_cast<int32_t*>(L.t.x64) + kWave;     // first point,
+    int32_t* const scn = reinterpret_cast<int32_t*>(L.t.y64);             // point count
     for (int c0 = 0; c0 < ncq; c0 += kWave) {
         // lane l: cell c0 + l -> its range of gbox records
         int cs = 0, cn = 0;
@@ -709,34 +708,33 @@ __device__ __forceinline__ void walk_g(const DevCloud& db, const Query<D>& q, Wa
                 if (cpre[k + st] <= j) k += st;
             const int pos = cst[k] + (j - cpre[k]);
             float key = 3e38f;
-            int tt = 0, tst = 0, tcnt = 0;
             if (j < total) {
                 const TileBox tb = db.gbox[pos];
                 key = gap2_box<D>(q, tb.c, tb.h);
-                tt = tb.pad;
-                tst = tb.start;
-                tcnt = tb.count;
+                stt[l] = tb.pad;
+                sst[l] = tb.start;
+                scn[l] = tb.count;
             }
             if (cnt) cnt->count(6);
-            int src = l;
-            wave_sort64(key, src);   // nearest-first; ties by lane (deterministic)
-            sk[l] = key;
-            stt[l] = __shfl(tt, src);
-            sst[l] = __shfl(tst, src);
-            scn[l] = __shfl(tcnt, src);
             wave_sync();
             const int nb = min(kWave, total - j0);
-            for (int m = 0; m < nb; ++m) {
-                const float km = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sk[m])));
-                if (!(km <= wb)) break;   // sorted: every later candidate is out of reach too
+            // nearest-first by repeated selection of the smallest remaining key (one DPP minimum per visit; no
+            // sort, only the key stays in a register, the records wait in LDS by lane)
+            uint64_t left = __ballot(l < nb && key <= wb);
+            while (left) {
+                const float km = wave_minf(((left >> l) & 1ull) ? key : 3e38f);
+                if (!(km <= wb)) break;   // every remaining candidate is out of reach
+                const int m = __ffsll((unsigned long long)__ballot(((left >> l) & 1ull) && key == km)) - 1;
+                left &= ~(1ull << m);
                 const float4 pv = load_rel(db, __builtin_amdgcn_readfirstlane(sst[m]), __builtin_amdgcn_readfirstlane(scn[m]));
                 if (visit_pre(__builtin_amdgcn_readfirstlane(stt[m]), &pv)) {
                     wb = wave_bound();
                     wbi = infl(wb);
+                    left &= __ballot(key <= wb);
                 }
             }
-            if (skin > 0.f) {   // the list: every candidate of this batch within the inflated bound, nearest-first
-                uint64_t cm = __ballot(l < nb && sk[l] <= wbi);
+            if (skin > 0.f) {   // the list: every candidate of this batch within the inflated bound
+                uint64_t cm = __ballot(l < nb && key <= wbi);
                 while (cm) {
                     const int m = __ffsll((unsigned long long)cm) - 1;
                     cm &= cm - 1;
