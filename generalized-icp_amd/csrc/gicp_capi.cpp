@@ -173,13 +173,6 @@ struct Cloud {
     uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows
     int32_t* nbi = nullptr;           // ... and their sorted indices
     bool graph_ready = false;
-    TileBox* gbox = nullptr;          // uniform tile grid (targets only): records in cell order
-    int32_t* gcell = nullptr;         // ... cell starts
-    bool grid_ready = false;
-    double glo[3] = {0, 0, 0}, ginv = 1.0;
-    int gdim[3] = {1, 1, 1};
-    float ghmax[3] = {0, 0, 0};
-    size_t cap_gbox = 0, cap_gcell = 0;
     bool cov_ready = false;
     int cov_shard = 0, cov_nshards = 1;  // whose tiles' covariances were computed (build_cloud)
 
@@ -213,10 +206,6 @@ struct Cloud {
         dfree(seed_tab);
         dfree(nbq);
         dfree(nbi);
-        dfree(gbox);
-        dfree(gcell);
-        cap_gbox = cap_gcell = 0;
-        grid_ready = false;
         cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
         cap_nbq = cap_nbi = cap_boxes = cap_seed = 0;
         n = 0;
@@ -237,14 +226,6 @@ struct Cloud {
         v.seed_shift = seed_shift;
         v.nbq = graph_ready ? nbq : nullptr;
         v.nbi = graph_ready ? nbi : nullptr;
-        v.gbox = grid_ready ? gbox : nullptr;
-        v.gcell = grid_ready ? gcell : nullptr;
-        for (int a = 0; a < 3; ++a) {
-            v.glo[a] = glo[a];
-            v.gdim[a] = gdim[a];
-            v.ghmax[a] = ghmax[a];
-        }
-        v.ginv = ginv;
         v.n = n;
         v.ntiles = ntiles;
         v.nblocks = nblocks;
@@ -569,69 +550,6 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
 
 // Build the device index of a cloud and the per-point covariances of all its tiles (a source shard
 // is a set of interleaved chunks, and the whole-cloud pass costs ~1 ms at 1M points).
-// The uniform tile grid of a target (k_corr's walk_g): cells of the largest tile extent (so a
-// tile's box reaches at most its neighbour cells), at most 2^22 of them (coarser cells for a sparse, vast
-// cloud); each tile listed once, in the cell of its box centre; the records in cell order.  Host-built from
-// the device's TileBox records (~1 MB at 1M points): a counting sort.
-void build_grid(Cloud& cl, hipStream_t st) {
-    const int nt = cl.ntiles, dim = cl.dim;
-    std::vector<TileBox> hb(nt);
-    HIPCHK(hipMemcpyAsync(hb.data(), cl.boxes, sizeof(TileBox) * nt, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    float hm[3] = {0.f, 0.f, 0.f};
-    for (const TileBox& b : hb)
-        for (int a = 0; a < dim; ++a) {
-            lo[a] = std::min(lo[a], b.c[a]);
-            hi[a] = std::max(hi[a], b.c[a]);
-            hm[a] = std::max(hm[a], b.h[a]);
-        }
-    double ext = 0.0;
-    for (int a = 0; a < dim; ++a) ext = std::max(ext, hi[a] - lo[a]);
-    double C = 2.0 * std::max({(double)hm[0], (double)hm[1], (double)hm[2]});
-    C = std::max(C, 1e-6 * (ext + 1.0));
-    int gd[3] = {1, 1, 1};
-    for (;;) {
-        double cells = 1.0;
-        for (int a = 0; a < dim; ++a) {
-            gd[a] = (int)std::floor((hi[a] - lo[a]) / C) + 1;
-            cells *= gd[a];
-        }
-        if (cells <= (double)(1 << 22)) break;
-        C *= 1.25;
-    }
-    const double inv = 1.0 / C;
-    const int64_t ncells = (int64_t)gd[0] * gd[1] * gd[2];
-    std::vector<int32_t> cid(nt), start(ncells + 1, 0);
-    for (int t = 0; t < nt; ++t) {
-        int ix[3] = {0, 0, 0};
-        for (int a = 0; a < dim; ++a)
-            ix[a] = std::min(gd[a] - 1, std::max(0, (int)std::floor((hb[t].c[a] - lo[a]) * inv)));
-        cid[t] = dim == 3 ? (ix[0] * gd[1] + ix[1]) * gd[2] + ix[2] : ix[0] * gd[1] + ix[1];
-        ++start[cid[t] + 1];
-    }
-    for (int64_t c = 0; c < ncells; ++c) start[c + 1] += start[c];
-    std::vector<TileBox> gb(nt);
-    std::vector<int32_t> fill(start.begin(), start.end() - 1);
-    for (int t = 0; t < nt; ++t) {   // tiles in index order within a cell (deterministic)
-        TileBox b = hb[t];
-        b.pad = t;
-        gb[fill[cid[t]]++] = b;
-    }
-    dreserve(cl.gbox, cl.cap_gbox, (size_t)nt);
-    dreserve(cl.gcell, cl.cap_gcell, (size_t)ncells + 1);
-    HIPCHK(hipMemcpyAsync(cl.gbox, gb.data(), sizeof(TileBox) * nt, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(cl.gcell, start.data(), sizeof(int32_t) * (ncells + 1), hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));   // the host vectors go out of scope
-    for (int a = 0; a < 3; ++a) {
-        cl.glo[a] = a < dim ? lo[a] : 0.0;
-        cl.gdim[a] = gd[a];
-        cl.ghmax[a] = a < dim ? hm[a] * (1.0f + 1e-6f) : 0.f;
-    }
-    cl.ginv = inv;
-    cl.grid_ready = true;
-}
-
 // Tiles of shard `shard` of `nshards` (the k_corr split: chunks of kShardChunk units of kCorrWaves tiles, dealt
 // round-robin), or all of them when nshards = 1.
 int shard_tile_count(int ntiles, int shard, int nshards) {
@@ -647,8 +565,7 @@ int shard_tile_count(int ntiles, int shard, int nshards) {
 // rank needs the whole cloud's index for the neighbourhoods, but only its own tiles' covariances); the other
 // rows read NaN.
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
-                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1,
-                 bool grid = false) {
+                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -666,7 +583,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
     cl.n = 0;   // buffers are kept (grow-only) and reused
     cl.cov_ready = false;
     cl.graph_ready = false;
-    cl.grid_ready = false;
     cl.dim = dim;
     cl.bits = dim == 3 ? 10 : 16;
     // one fused, branch-free pass: bounds and the finiteness test (v - v is NaN for NaN and +-inf)
@@ -773,10 +689,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         HIPCHK(hipStreamSynchronize(st));
         std::memcpy(&cl.rho, &rho_bits, sizeof(float));
         tick("tiles");
-        if (grid) {
-            build_grid(cl, st);
-            tick("grid");
-        }
 
         // surface covariances (gicp.py:19-35), of this rank's tiles when sharded
         const int qb = 0, qe = shard_tile_count(cl.ntiles, cov_shard, cov_nshards);
@@ -1351,8 +1263,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs, c->bs, c->stream, false, 0, 1,
-                    true);
+        build_cloud(c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs, c->bs, c->stream);
         if (c->src.n) reset_tile_state(c);
     });
 }
@@ -1713,8 +1624,7 @@ int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const 
         g.th = std::thread([gp, M, dim, graph, dev] {
             try {
                 HIPCHK(hipSetDevice(dev));
-                // (a target: with the tile grid k_corr walks)
-                build_cloud(gp->cl, gp->bs.h_pinned, M, dim, gp->p, graph, gp->bs, gp->stream, true, 0, 1, true);
+                build_cloud(gp->cl, gp->bs.h_pinned, M, dim, gp->p, graph, gp->bs, gp->stream, true);
             } catch (const Fail& f) {
                 gp->rc = f.code;
                 gp->err = f.msg;
@@ -1750,7 +1660,6 @@ int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
         g.cl.n = 0;
         g.cl.cov_ready = false;
         g.cl.graph_ready = false;
-        g.cl.grid_ready = false;
         c->ptgt = g.p;
         c->top_ready = false;
         if (c->src.n) set_shard(c, shard, nshards);

@@ -94,16 +94,6 @@ struct DevCloud {
     // entry k (-1 unused).
     const uint4* nbq;         // [n][8]
     const int32_t* nbi;       // [n][kGraphK]
-    // uniform grid of the tiles (target only; null when not built), DESIGN.md §3d: cell (ix, iy, iz) =
-    // floor((centre - glo) * ginv) holds the tiles whose box centre lies in it, as the TileBox records
-    // gbox[gcell[cid] .. gcell[cid + 1]) (the record's pad = the tile index), cid = (ix gdim1 + iy) gdim2 + iz;
-    // every tile's half-extent is <= ghmax per axis
-    const TileBox* gbox;      // [ntiles] in cell order
-    const int32_t* gcell;     // [ncells + 1]
-    double glo[3];
-    double ginv;              // 1 / cell size
-    int32_t gdim[3];
-    float ghmax[3];
     int64_t n;
     int32_t ntiles;
     int32_t nblocks;

@@ -630,122 +630,6 @@ __device__ __forceinline__ void walk_c(const DevCloud& db, const Query<D>& q, in
     }
 }
 
-// k_corr's full walk over the target's uniform tile grid instead of the box hierarchy: the
-// cells within reach of the wave box (the inflated bound at the start, plus the largest tile half-extent)
-// are requested at once, one lane per cell (their tile ranges), then their tiles' TileBox records, one lane
-// per tile, and the candidates are visited nearest-first (box gap to the wave box), each while it is still
-// within the shrinking bound -- 3 round trips before the first visit instead of the hierarchy's ~10, and
-// fewer visits (the bound shrinks fastest nearest-first).  Every tile within the initial reach is a candidate
-// (its centre's cell is in the range), so the walk visits whatever else it needs: the results are identical.
-// The cells are taken 64 per round (one round unless the reach is large against the cells).  The candidates'
-// records wait in the wave's LDS (the fp64 staging area, free during the walk), only their keys in registers.
-template <int D, class VisitPre, class WB, class Collect, class Cnt = NoCount>
-__device__ __forceinline__ void walk_g(const DevCloud& db, const Query<D>& q, WaveLds& L, VisitPre&& visit_pre,
-                                       WB&& wave_bound, float skin, Collect&& collect, Cnt* cnt = nullptr) {
-    const int l = lane_id();
-    auto infl = [&](float w) -> float {
-        if (skin <= 0.f || w < 0.f) return w;
-        const float r = __builtin_amdgcn_sqrtf(w) * 1.0001f + skin;
-        return r * r;
-    };
-    float wb = wave_bound();
-    if (wb < 0.f) return;   // no lane searches
-    float wbi = infl(wb);
-    // reach per axis, in cells: the wave box, the bound (rounded up), the largest tile half-extent
-    const float reach = __builtin_amdgcn_sqrtf(wbi) * 1.0001f + 1e-6f;
-    const float ginv = (float)db.ginv;
-    int lo[3] = {0, 0, 0}, nc[3] = {1, 1, 1};
-    int ncq = 1;
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-        const float oc = (float)((q.ow[a] - db.glo[a]) * db.ginv);   // the wave centre's cell coordinate
-        const float ec = (q.ew[a] + reach + db.ghmax[a]) * ginv * 1.0001f + 1e-3f;
-        const int a0 = max(0, (int)floorf(oc - ec));
-        const int a1 = min(db.gdim[a] - 1, (int)floorf(oc + ec));
-        lo[a] = __builtin_amdgcn_readfirstlane(a0);
-        nc[a] = __builtin_amdgcn_readfirstlane(max(0, a1 - a0 + 1));
-        ncq *= nc[a];
-    }
-    int32_t* const stt = reinterpret_cast<int32_t*>(L.t.x64);             // candidate of lane l: tile,
-    int32_t* const sst = reinterpret_cast<int32_t*>(L.t.x64) + kWave;     // first point,
-    int32_t* const scn = reinterpret_cast<int32_t*>(L.t.y64);             // point count
-    for (int c0 = 0; c0 < ncq; c0 += kWave) {
-        // lane l: cell c0 + l -> its range of gbox records
-        int cs = 0, cn = 0;
-        if (c0 + l < ncq) {
-            int c = c0 + l, ix = 0, iy = 0, iz = 0;
-            if (D == 3) {
-                iz = c % nc[2];
-                c /= nc[2];
-            }
-            iy = c % nc[1];
-            ix = c / nc[1];
-            const int cid = D == 3 ? ((lo[0] + ix) * db.gdim[1] + lo[1] + iy) * db.gdim[2] + lo[2] + iz
-                                   : (lo[0] + ix) * db.gdim[1] + lo[1] + iy;
-            cs = db.gcell[cid];
-            cn = db.gcell[cid + 1] - cs;
-        }
-        // exclusive prefix of the counts over the lanes
-        int pre = cn;
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-            const int v = __shfl_up(pre, o);
-            if (l >= o) pre += v;
-        }
-        const int total = __builtin_amdgcn_readlane(pre, kWave - 1);
-        // the round's cell ranges wait in LDS while its candidates are visited (not in registers)
-        int32_t* const cpre = L.t.perm;
-        int32_t* const cst = reinterpret_cast<int32_t*>(L.t.z64);
-        cpre[l] = pre - cn;
-        cst[l] = cs;
-        wave_sync();
-        for (int j0 = 0; j0 < total; j0 += kWave) {
-            // lane l: candidate j = j0 + l, in the cell k with pre[k] <= j < pre[k] + cnt[k] (largest such k)
-            const int j = j0 + l;
-            int k = 0;
-#pragma unroll
-            for (int st = kWave / 2; st > 0; st >>= 1)
-                if (cpre[k + st] <= j) k += st;
-            const int pos = cst[k] + (j - cpre[k]);
-            float key = 3e38f;
-            if (j < total) {
-                const TileBox tb = db.gbox[pos];
-                key = gap2_box<D>(q, tb.c, tb.h);
-                stt[l] = tb.pad;
-                sst[l] = tb.start;
-                scn[l] = tb.count;
-            }
-            if (cnt) cnt->count(6);
-            wave_sync();
-            const int nb = min(kWave, total - j0);
-            // nearest-first by repeated selection of the smallest remaining key (one DPP minimum per visit; no
-            // sort, only the key stays in a register, the records wait in LDS by lane)
-            uint64_t left = __ballot(l < nb && key <= wb);
-            while (left) {
-                const float km = wave_minf(((left >> l) & 1ull) ? key : 3e38f);
-                if (!(km <= wb)) break;   // every remaining candidate is out of reach
-                const int m = __ffsll((unsigned long long)__ballot(((left >> l) & 1ull) && key == km)) - 1;
-                left &= ~(1ull << m);
-                const float4 pv = load_rel(db, __builtin_amdgcn_readfirstlane(sst[m]), __builtin_amdgcn_readfirstlane(scn[m]));
-                if (visit_pre(__builtin_amdgcn_readfirstlane(stt[m]), &pv)) {
-                    wb = wave_bound();
-                    wbi = infl(wb);
-                    left &= __ballot(key <= wb);
-                }
-            }
-            if (skin > 0.f) {   // the list: every candidate of this batch within the inflated bound
-                uint64_t cm = __ballot(l < nb && key <= wbi);
-                while (cm) {
-                    const int m = __ffsll((unsigned long long)cm) - 1;
-                    cm &= cm - 1;
-                    collect(__builtin_amdgcn_readfirstlane(stt[m]));
-                }
-            }
-            wave_sync();
-        }
-    }
-}
-
 __device__ __forceinline__ void stage_f64(const DevCloud& db, const TileInfo& ti, WaveLds& L) {
     const int l = lane_id();
     double4 v;
@@ -1527,8 +1411,23 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         const bool lists = A.use_lists != 0;
 
-        // the fp64 fallback's hierarchy walk starts at last pass's best target tile (if any)
-        const int seed = hint0 >= 0 && hint0 < tg.ntiles ? hint0 : -1;
+        // seed: last pass's best target tile for this source tile, else the Morton neighbour
+        int seed = hint0;
+        if (seed < 0 || seed >= tg.ntiles) {
+            const uint32_t code = morton_code(q.ow, D, tg.lo, tg.scale, tg.bits);
+            int lo = 0, hi = tg.ntiles - 1;
+            if (tg.seed_tab) {   // the bucket's range: both ends in one round trip
+                const uint32_t b = code >> tg.seed_shift;
+                lo = tg.seed_tab[b];
+                hi = tg.seed_tab[b + 1];
+            }
+            while (lo < hi) {  // last tile whose first code <= code
+                const int mid = (lo + hi + 1) >> 1;
+                if (tg.tile_code[mid] <= code) lo = mid;
+                else hi = mid - 1;
+            }
+            seed = lo;
+        }
 
         // displacement bound of any point of this source tile between the pose of pass `bp` (pose ring)
         // and this pass: |dR c + dt| + ||dR||_F rho; < 0 if that pose has left the ring
@@ -1894,7 +1793,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 if (l == ncol) cent = Tt;
                 ++ncol;
             };
-            walk_g<D>(tg, q, L, visit_pre, [&]() { return wave_maxf(lb); }, lists ? skin : 0.f, collect, &S);
+            walk_c<D>(tg, q, seed, visit_pre, [&]() { return wave_maxf(lb); }, lists ? skin : 0.f,
+                      collect, &S);
             if (lists) {
                 const float wbf = wave_maxf(lb);
                 const float r = ncol <= kListMax ? __builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 0.9999f + skin : 0.f;
@@ -2029,7 +1929,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     visit64(__builtin_amdgcn_readlane(ent, k));
                 }
             } else {
-                traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });   // seed: uniform
+                traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
             }
             if (amb) j = bj;
             // exact certificate of a re-resolved lane: every row within lim was scanned in fp64, so
