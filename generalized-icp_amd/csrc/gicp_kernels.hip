@@ -1522,35 +1522,56 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
                     float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f, rho = 0.f;
                     int bk = -1;
-                    auto entry = [&](int k) {
-                        int c3[3];
+                    auto coords = [&](int k, float* c) {
 #pragma unroll
                         for (int a = 0; a < 3; ++a) {
                             const int p = 4 + 3 * k + a;   // int16 slot (2 header dwords = 4 slots)
-                            c3[a] = (p & 1) ? ((int)w[p >> 1] >> 16) : (((int)(w[p >> 1] << 16)) >> 16);
+                            c[a] = (float)((p & 1) ? ((int)w[p >> 1] >> 16) : (((int)(w[p >> 1] << 16)) >> 16));
                         }
-                        const float dx = fmaf(-sc, (float)c3[0], qr[0]);
-                        const float dy = fmaf(-sc, (float)c3[1], qr[1]);
-                        const float dz = fmaf(-sc, (float)c3[2], qr[2]);
-                        // (an unused entry repeats a real one, k_graph_pack: no validity test here)
-                        const float dd = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                        if (dd < b1) {
-                            b2 = b1;
-                            b1 = dd;
+                    };
+                    // the winner so far and the runner-up (non-negative floats order like their bits: the
+                    // runner-up is the median of {winner, runner-up, new}, one v_med3_u32, no NaN canonicalisation)
+                    auto upd = [&](float dd, float dx, float dy, float dz, int k) {
+                        const unsigned ud = __float_as_uint(dd), u1 = __float_as_uint(b1);
+                        const bool lt = ud < u1;
+                        b2 = __uint_as_float(umed3(u1, __float_as_uint(b2), ud));
+                        b1 = __uint_as_float(min(u1, ud));
+                        if (lt) {
                             bk = k;
                             bx = dx;
                             by = dy;
                             bz = dz;
-                        } else {   // (non-negative floats order like their bits: v_min_u32, no NaN canonicalisation)
-                            b2 = __uint_as_float(min(__float_as_uint(b2), __float_as_uint(dd)));
                         }
+                    };
+                    // (an unused entry repeats a real one, k_graph_pack: no validity test here)
+                    auto entry = [&](int k) {
+                        float c[3];
+                        coords(k, c);
+                        const float dx = fmaf(-sc, c[0], qr[0]);
+                        const float dy = fmaf(-sc, c[1], qr[1]);
+                        const float dz = fmaf(-sc, c[2], qr[2]);
+                        upd(fmaf(dx, dx, fmaf(dy, dy, dz * dz)), dx, dy, dz, k);
                         if (k == kRowSplit - 1) {   // |offset| of the first half's last entry (quantised)
-                            const float ox = sc * (float)c3[0], oy = sc * (float)c3[1], oz = sc * (float)c3[2];
+                            const float ox = sc * c[0], oy = sc * c[1], oz = sc * c[2];
                             rho = __builtin_amdgcn_sqrtf(fmaf(ox, ox, fmaf(oy, oy, oz * oz)));
                         }
                     };
+                    // entries k and k + 1 on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: half the distance VALU)
+                    auto entry2 = [&](int k) {
+                        float ca[3], cb[3];
+                        coords(k, ca);
+                        coords(k + 1, cb);
+                        const f2v ms = {-sc, -sc};
+                        const f2v dx = __builtin_elementwise_fma(ms, f2v{ca[0], cb[0]}, f2v{qr[0], qr[0]});
+                        const f2v dy = __builtin_elementwise_fma(ms, f2v{ca[1], cb[1]}, f2v{qr[1], qr[1]});
+                        const f2v dz = __builtin_elementwise_fma(ms, f2v{ca[2], cb[2]}, f2v{qr[2], qr[2]});
+                        const f2v dd = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+                        upd(dd.x, dx.x, dy.x, dz.x, k);
+                        upd(dd.y, dx.y, dy.y, dz.y, k + 1);
+                    };
 #pragma unroll
-                    for (int k = 0; k < kRowSplit; ++k) entry(k);
+                    for (int k = 0; k + 1 < kRowSplit; k += 2) entry2(k);
+                    if (kRowSplit & 1) entry(kRowSplit - 1);
                     const float d0 = __builtin_amdgcn_sqrtf(d0s);
                     // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
                     const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
@@ -1564,7 +1585,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         if (need2) {
                             load_half(4);
 #pragma unroll
-                            for (int k = kRowSplit; k < kGraphK; ++k) entry(k);
+                            for (int k = kRowSplit; k + 1 < kGraphK; k += 2) entry2(k);
+                            if ((kGraphK - kRowSplit) & 1) entry(kGraphK - 1);
                         }
                     }
                     if (!need2) b2 = fminf(b2, lc * lc);
