@@ -324,7 +324,6 @@ struct gicp_ctx {
     int unit_map = 0;                 // k_corr workgroup -> unit map (CorrArgs::unit_map, GICP_UNIT_MAP)
     int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
-    int scramble_iters = 0;           // ... of which the first ones take the chunks in scrambled order (GICP_SCRAMBLE_ITERS)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
@@ -819,17 +818,6 @@ double accept_d2_max(double dc) {
     return x;
 }
 
-// A stride coprime to the number of full chunks of C units (k_corr's scrambled chunk order), near the golden
-// section of it so consecutive chunks land far apart; 0 when there is nothing to scramble.
-int scramble_stride(int nunits, int C) {
-    const int nch = nunits / (8 * C) * 8;
-    if (nch < 3) return 0;
-    int s = (int)(0.6180339887 * nch) | 1;
-    auto gcd = [](int a, int b) { while (b) { const int t = a % b; a = b; b = t; } return a; };
-    while (gcd(s, nch) != 1) s += 2;
-    return s % nch;
-}
-
 // kernel arguments of a pass (the pose comes from the device state)
 CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     const int d = c->src.dim;
@@ -1139,7 +1127,6 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_UNIT_MAP")) c->unit_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("GICP_SCRAMBLE_ITERS")) c->scramble_iters = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -1488,7 +1475,6 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                 const int it = enq + b;
                 CorrArgs a = corr_args(c, 0);
                 if (it < c->moving_iters) a.unit_map = c->moving_map;
-                if (it < c->scramble_iters && a.unit_map > 0) a.unit_stride = scramble_stride(grid, a.unit_map);
                 if (tk > 0) {   // det(W) of every point, for this iteration's top-k rows (gicp.py:170)
                     a.dbg_det = c->d_dbg_det;
                     a.top_tgt = c->d_top_tgt;

@@ -206,7 +206,6 @@ struct CorrArgs {
     // workgroup -> unit map: 0 = XCD stripes (XCD x takes the contiguous eighth x), C > 0 = chunks of C
     // units dealt round-robin to the XCDs (1 = identity)
     int32_t unit_map;
-    int32_t unit_stride;      // > 0 (with unit_map > 0): chunk c is processed as chunk (c unit_stride) mod chunks
     IterState* state;         // pose in, statistics out
     uint32_t* tickets;        // [kMaxGroups + 1] arrival counters, zero between launches (self-resetting)
     double* gpart;            // [kMaxGroups][nstat_ext] group partials

@@ -1325,13 +1325,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (unit < 8 * q8) unit = (unit & 7) * q8 + (unit >> 3);
     } else {   // the k-th workgroup of XCD x takes unit k % C of the XCD's (k / C)-th chunk of C units
         const int C = A.unit_map, full = nunits / (8 * C) * (8 * C);
-        if (unit < full) {
-            int chunk = ((unit >> 3) / C) * 8 + (unit & 7);
-            // scrambled chunk order (unit_stride coprime to the chunk count): the spatially clustered
-            // expensive chunks spread over the launch instead of ending it
-            if (A.unit_stride > 0) chunk = (int)(((int64_t)chunk * A.unit_stride) % (full / C));
-            unit = chunk * C + (unit >> 3) % C;
-        }
+        if (unit < full) unit = (((unit >> 3) / C) * 8 + (unit & 7)) * C + (unit >> 3) % C;
     }
     unit = __builtin_amdgcn_readfirstlane(unit);
     // this rank's unit -> the cloud's unit (shards interleaved by chunks, gicp_internal.h)
