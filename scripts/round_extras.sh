@@ -17,3 +17,7 @@ for f in bench_c2 bench_2d_1m bench_2d_100k; do python3 -c "import json;d=json.l
 cat $OUT/bench_odometry_staged.json | head -c 600; echo
 timeout -k 10 300 python scripts/full_output_cost.py > $OUT/full_output_cost.json 2> $OUT/foc.err || { echo full_output_cost failed; tail $OUT/foc.err; exit 1; }
 cat $OUT/full_output_cost.json
+timeout -k 10 300 python bench_small.py > $OUT/bench_c1.json 2> $OUT/c1.err || { echo c1 failed; exit 1; }
+timeout -k 10 300 python3 bench.py --shard-sim 8 --no-cpu-baseline > $OUT/bench_shard_sim8.json 2> $OUT/sim8.err || { echo sim8 failed; exit 1; }
+timeout -k 10 300 python3 bench.py --gpus 2 --share-gpu --no-cpu-baseline --steps 20 > $OUT/share2.log 2> $OUT/share2.err || { echo share failed; exit 1; }
+tail -1 $OUT/share2.log > $OUT/bench_share2_peer.json

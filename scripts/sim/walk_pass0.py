@@ -122,9 +122,10 @@ def gap2(c1, h1, c2, h2):
 
 class Wave:
     def __init__(self, w):
-        self.p = sq[w]
+        p = sq[w]
+        self.p = p[p[:, 0] < 1e8]          # the tile's points (padding rows excluded, as k_corr's invalid lanes)
         self.c, self.h = sC[w], sH[w]
-        self.best = np.full(64, R0 * R0)
+        self.best = np.full(len(self.p), R0 * R0)
         self.rt = self.visits = self.scanned = self.rows = 0
 
     def wb(self):
@@ -177,6 +178,82 @@ def hier(w):
     return wv
 
 
+def hier2(w, frac=0.5):
+    """hier with a two-box candidate test: after the seed visit the lanes whose bound reaches past frac x the
+    largest radius form a 'far' box; a block / tile is a candidate if it is within the near lanes' bound of
+    the wave box or within the far lanes' bound of the far box (bounds per class, updated as they shrink)"""
+    wv = Wave(w)
+    seed = seed_of(wv)
+    wv.rt += 3
+    wv.visit(seed)
+    rmax = np.sqrt(wv.wb())
+    big = wv.best > (frac * rmax) ** 2
+    if big.any():
+        pb = wv.p[big]
+        fc, fh = (pb.min(0) + pb.max(0)) / 2, (pb.max(0) - pb.min(0)) / 2
+    else:
+        fc, fh = wv.c, wv.h
+
+    def cand(c, h):
+        near = wv.best[~big].max() if (~big).any() else -1.0
+        far = wv.best[big].max() if big.any() else -1.0
+        return (gap2(wv.c, wv.h, c, h) <= near) | (gap2(fc, fh, c, h) <= far)
+
+    for s0 in range(0, NS, 64):
+        wv.rt += 1
+        sl = np.arange(s0, min(NS, s0 + 64))
+        for s in sl[cand(sbC[sl], sbH[sl])]:
+            if not cand(sbC[s], sbH[s]):
+                continue
+            wv.rt += 1
+            bl = np.arange(64 * s, min(NB, 64 * s + 64))
+            for b in bl[cand(bC[bl], bH[bl])]:
+                if not cand(bC[b], bH[b]):
+                    continue
+                wv.rt += 1
+                tl = np.arange(64 * b, min(NT, 64 * b + 64))
+                for t in tl[cand(tC[tl], tH[tl]) & (tl != seed)]:
+                    if cand(tC[t], tH[t]):
+                        wv.visit(t)
+    return wv
+
+
+def hier4(w):
+    """hier with the candidate test against the source tile's 4 sub-boxes (16 lanes each), each with its own
+    lanes' bound: a tile / block is a candidate if it is within reach of any sub-box"""
+    wv = Wave(w)
+    seed = seed_of(wv)
+    wv.rt += 3
+    wv.visit(seed)
+    n = len(wv.p)
+    groups = [np.arange(g * 16, min(n, g * 16 + 16)) for g in range(4) if g * 16 < n]
+    boxes = [((wv.p[gi].min(0) + wv.p[gi].max(0)) / 2, (wv.p[gi].max(0) - wv.p[gi].min(0)) / 2) for gi in groups]
+
+    def cand(c, h):
+        ok = False
+        for gi, (bc, bh) in zip(groups, boxes):
+            ok = ok | (gap2(bc, bh, c, h) <= wv.best[gi].max())
+        return ok
+
+    for s0 in range(0, NS, 64):
+        wv.rt += 1
+        sl = np.arange(s0, min(NS, s0 + 64))
+        for s in sl[cand(sbC[sl], sbH[sl])]:
+            if not cand(sbC[s], sbH[s]):
+                continue
+            wv.rt += 1
+            bl = np.arange(64 * s, min(NB, 64 * s + 64))
+            for b in bl[cand(bC[bl], bH[bl])]:
+                if not cand(bC[b], bH[b]):
+                    continue
+                wv.rt += 1
+                tl = np.arange(64 * b, min(NT, 64 * b + 64))
+                for t in tl[cand(tC[tl], tH[tl]) & (tl != seed)]:
+                    if cand(tC[t], tH[t]):
+                        wv.visit(t)
+    return wv
+
+
 def grid(w, seeded=True, skin=0.0):
     wv = Wave(w)
     seed = -1
@@ -207,13 +284,12 @@ def grid(w, seeded=True, skin=0.0):
 
 
 waves = rng.choice(len(sC), size=NW, replace=False)
-for name, fn in (("hier", hier), ("grid", grid), ("grid_ns", lambda w: grid(w, False)),
-                 ("grid_ns_skin", lambda w: grid(w, False, 0.1))):
+for name, fn in (("hier", hier), ("hier4", hier4)):
     t0 = time.time()
     res = [fn(int(w)) for w in waves]
     rt = np.array([x.rt for x in res]); vi = np.array([x.visits for x in res])
     scn = np.array([x.scanned for x in res]); rows = np.array([x.rows for x in res])
-    print(f"{name:7s} cell {CELL:.2f}: round trips {rt.mean():6.1f} (p90 {np.percentile(rt, 90):4.0f})  visits {vi.mean():5.1f}"
+    print(f"{name:7s} cell {CELL:.2f}: round trips {rt.mean():6.1f} (p90 {np.percentile(rt, 90):4.0f}, p99 {np.percentile(rt, 99):4.0f})  visits {vi.mean():5.1f} (p99 {np.percentile(vi, 99):4.0f})"
           f"  scanned {scn.mean():5.1f}  rows {rows.mean():6.1f}   [{time.time() - t0:.0f} s]", flush=True)
     if hasattr(res[0], "ncand"):
         nc = np.array([x.ncand for x in res]); ncl = np.array([x.ncells for x in res])
