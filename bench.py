@@ -334,6 +334,10 @@ def main():
         "comm_ranks": comm_ranks,
         "comm": comm_kind,
         "comm_fallback": peer_note,
+        "exchange_us": None if comm_kind != "peer" else
+        {"mean": res["exchange_us_mean"], "min": res["exchange_us_min"],
+         "note": "rank 0's final workgroup per launch of the timed call: its stores into every rank's area until "
+                 "every rank's flag arrived (includes waiting for the slower rank)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "traffic_note": traffic_note,

@@ -1453,6 +1453,7 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
         hs.pairs_total = 0.0;
         hs.converged_at = -1;
         HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(&c->d_state->xchg_sum, 0, 3 * sizeof(double), st));   // this call's exchange timing
         const int grid = corr_grid(c->src.ntiles, c->shard, c->nshards);
         const bool timing = res != nullptr && prm.timing_stride >= 0;   // < 0: no timing events
         const auto t0 = std::chrono::steady_clock::now();
@@ -1580,6 +1581,13 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
             r.corr_kernel_ms_sampled = corr_ms;
             r.corr_samples = samples;
             r.mse = hs.mse;
+            if (hs.xchg_n > 0.0) {   // wall-clock ticks -> us
+                int khz = 0;
+                HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+                const double us = 1e3 / (khz > 0 ? khz : 100000);
+                r.exchange_us_mean = hs.xchg_sum / hs.xchg_n * us;
+                r.exchange_us_min = hs.xchg_min * us;
+            }
             *res = r;
         }
     });

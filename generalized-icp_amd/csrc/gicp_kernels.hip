@@ -2277,13 +2277,23 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     double hv = 0.0;
     if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     sum_rows(A.gpart, 0, ng, s_sum);
-    if (A.peer.n > 1 && !peer_exchange<NSX>(A.peer, s_sum)) {   // the sum over ranks, in-kernel
-        if (threadIdx.x == 0) {   // a peer never arrived: fail the call, later launches exit at once
-            A.state->solve_fail = 2;
-            A.state->converged = 1;
-            __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (A.peer.n > 1) {   // the sum over ranks, in-kernel
+        const uint64_t x0 = (uint64_t)wall_clock64();
+        if (!peer_exchange<NSX>(A.peer, s_sum)) {
+            if (threadIdx.x == 0) {   // a peer never arrived: fail the call, later launches exit at once
+                A.state->solve_fail = 2;
+                A.state->converged = 1;
+                __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
         }
-        return;
+        if (threadIdx.x == 0) {   // how long this rank's exchange took (its stores to every rank's flags arriving)
+            const double dt = (double)((uint64_t)wall_clock64() - x0);
+            const double m = A.state->xchg_min;
+            A.state->xchg_sum += dt;
+            A.state->xchg_min = m > 0.0 ? fmin(m, dt) : dt;
+            A.state->xchg_n += 1.0;
+        }
     }
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -73,6 +73,8 @@ class Result(C.Structure):
         ("corr_kernel_ms_sampled", C.c_double),
         ("corr_samples", C.c_int32),
         ("pad2", C.c_int32),
+        ("exchange_us_mean", C.c_double),
+        ("exchange_us_min", C.c_double),
     ]
 
     def as_dict(self):

@@ -109,6 +109,8 @@ typedef struct gicp_result {
     double corr_kernel_ms_sampled;  /* sum of the event-timed correspondence launches ... */
     int32_t corr_samples;           /* ... and how many there were */
     int32_t pad2;
+    double exchange_us_mean;        /* peer exchange (gicp_peer_init): mean / minimum time the final workgroup spent */
+    double exchange_us_min;         /* in the exchange per launch of this call (its stores to every rank's arrival) */
 } gicp_result;
 
 /* Optional caller-allocated per-point outputs of one pass, ORIGINAL source
