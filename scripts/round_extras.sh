@@ -21,3 +21,6 @@ timeout -k 10 300 python bench_small.py > $OUT/bench_c1.json 2> $OUT/c1.err || {
 timeout -k 10 300 python3 bench.py --shard-sim 8 --no-cpu-baseline > $OUT/bench_shard_sim8.json 2> $OUT/sim8.err || { echo sim8 failed; exit 1; }
 timeout -k 10 300 python3 bench.py --gpus 2 --share-gpu --no-cpu-baseline --steps 20 > $OUT/share2.log 2> $OUT/share2.err || { echo share failed; exit 1; }
 tail -1 $OUT/share2.log > $OUT/bench_share2_peer.json
+timeout -k 10 300 python3 bench.py --gpus 2 --share-gpu --no-cpu-baseline --n 20000 --steps 100 > $OUT/share2s.log 2> $OUT/share2s.err || { echo share small failed; exit 1; }
+tail -1 $OUT/share2s.log > $OUT/bench_share2_peer_20k.json
+timeout -k 10 300 python3 bench.py --shard-sim 2 --no-cpu-baseline --n 20000 --steps 100 > $OUT/bench_shard_sim2_20k.json 2> $OUT/sim2s.err || { echo sim2 small failed; exit 1; }
