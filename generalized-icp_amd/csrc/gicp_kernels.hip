@@ -2176,6 +2176,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #endif
 #ifndef GICP_TIMELINE
         o[16] = S.rt0;                                   // 100 MHz realtime: wave start / end
+#else
+        o[0] = (unsigned)T;                              // the wave's source tile, its radius and size
+        o[1] = __float_as_uint(st.radius);
+        o[2] = (unsigned)st.count;
 #endif
         o[17] = __builtin_amdgcn_s_memrealtime();
         o[18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
