@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--n", "--points", dest="n", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -103,16 +103,18 @@ def launch_ranks(a):
                   "refusing to run (no fallback to fewer GPUs)", file=sys.stderr)
             return 2
     import subprocess
+    # (the launcher's own parser reads every "--x" token, the script's too: "--n" would be an ambiguous
+    # prefix of its options, so it travels as --points)
+    args = ["--points" + x[3:] if x == "--n" or x.startswith("--n=") else x for x in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
-           *sys.argv[1:]]
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *args]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC: RCCL's only mode on this driver
     env.setdefault("OMP_NUM_THREADS", "1")
     return subprocess.run(cmd, env=env).returncode
 
 
-def dry_run(world, rank, local):
+def dry_run(world, rank, local, points):
     """Rank plumbing only (CPU, gloo): every rank reports itself, rank 0 prints the gathered list."""
     import torch.distributed as dist
     if world > 1:
@@ -123,7 +125,7 @@ def dry_run(world, rank, local):
     else:
         got = [{"rank": rank, "local_rank": local, "world_size": world}]
     if rank == 0:
-        print(json.dumps({"dry_run": True, "world_size": world, "ranks": got}))
+        print(json.dumps({"dry_run": True, "world_size": world, "ranks": got, "points": points}))
 
 
 def workload(n, dim):
@@ -199,7 +201,7 @@ def main():
               file=sys.stderr)
         sys.exit(2)
     if a.dry_run:
-        dry_run(world, rank, local)
+        dry_run(world, rank, local, a.n)
         return
     dist = None
     dev = 0 if a.share_gpu else local

@@ -35,6 +35,15 @@ def test_dry_run_spawns_two_ranks():
     assert all(x["world_size"] == 2 for x in d["ranks"])
 
 
+def test_point_count_reaches_the_ranks():
+    """--n is an ambiguous prefix of the launcher's own options (its parser reads the script's tokens
+    too): the ranks still receive it."""
+    for args in (["--n", "20000"], ["--n=20000"], ["--points", "20000"]):
+        r = _run(["--gpus", "2", "--dry-run", *args])
+        assert r.returncode == 0, r.stderr
+        assert _json_line(r.stdout)["points"] == 20000
+
+
 def test_dry_run_one_rank_needs_no_launcher():
     r = _run(["--gpus", "1", "--dry-run"])
     assert r.returncode == 0, r.stderr
