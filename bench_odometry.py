@@ -85,7 +85,10 @@ def main():
                    "trajectory": "0.5 m and 0.5 deg yaw per frame (+-10 %), SURVEY.md 8(d)",
                    "max_iterations": a.max_iterations, "fixed_iterations": bool(a.fixed), **kw},
         "frame_error": {"rot_rad_median": float(np.median(errs[:, 0])), "rot_rad_max": float(errs[:, 0].max()),
-                        "trans_median": float(np.median(errs[:, 1])), "trans_max": float(errs[:, 1].max())},
+                        "trans_median": float(np.median(errs[:, 1])), "trans_max": float(errs[:, 1].max()),
+                        "note": "model-limited: the reference's covariance model (eps (I - n n^T) + 0.1 eps n n^T, "
+                                "SURVEY.md 8.A) under-registers the yaw step on these scans; the GPU equals the "
+                                "oracle frame by frame (tests/test_odometry.py::test_full_size_stream_per_frame_vs_oracle)"},
         "drift": {"trans": float(np.linalg.norm(est_end[:3, 3] - true_end[:3, 3])),
                   "rot_rad": S.rotation_angle_error(est_end, true_end),
                   "path_length": float(sum(np.linalg.norm(frames[k][1][:3, 3] - frames[k - 1][1][:3, 3])

@@ -370,8 +370,10 @@ def inner_gn(s, q, W, idx, T0, max_iter=100, tol=1e-14):
 def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_distance_correspondence=150,
          max_distance_nearest_neighbors=50, inner=None, k=None, source_cov="auto", fixed_iterations=False,
          record=False, T0=None, method="plane_to_plane", transformation_epsilon=0.0, rotation_epsilon=0.0,
-         euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0):
+         euclidean_fitness_epsilon=0.0, mse_relative_epsilon=0.0, workers=1):
     """Oracle of gicp() returning the reference's 7-tuple (+ records if asked).
+
+    workers: cKDTree query threads (the neighbourhoods and the correspondences; results are the same).
 
     method / the PCL-style epsilons: the §8(f) extensions (weights_model, pcl_stop); defaults are the
     reference's behaviour.
@@ -392,7 +394,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     if source_cov == "auto":
         source_cov = "recompute" if d == 2 else "rotate"
     d_c, d_n = max_distance_correspondence, max_distance_nearest_neighbors
-    tgt_cov, tgt_cnt = covariances(tgt, d_n, k)
+    tgt_cov, tgt_cnt = covariances(tgt, d_n, k, workers=workers)
     pcl = dict(transformation_epsilon=transformation_epsilon, rotation_epsilon=rotation_epsilon,
                euclidean_fitness_epsilon=euclidean_fitness_epsilon, mse_relative_epsilon=mse_relative_epsilon)
     use_pcl = transformation_epsilon > 0 or euclidean_fitness_epsilon > 0 or mse_relative_epsilon > 0
@@ -403,18 +405,18 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
     all_T = [T]
     offset = np.array([T[0, 2], T[1, 2], np.arctan2(T[1, 0], T[0, 0])]) if d == 2 else None
     last = np.inf
-    init_src_cov, _ = covariances(src, d_n, k)
+    init_src_cov, _ = covariances(src, d_n, k, workers=workers)
     hw_s, hw_t, all_src_cov, recs = [], [], [], []
     converged_at = -1
     for it in range(max_iterations):
         moved = apply_transformation(src, T)
         if source_cov == "recompute":
-            cs, _ = covariances(moved, d_n, k)
+            cs, _ = covariances(moved, d_n, k, workers=workers)
         else:
             R = T[:d, :d]
             cs = np.einsum("ab,nbc,dc->nad", R, init_src_cov, R)
         all_src_cov.append(cs)
-        idx, dist = correspondences(moved, tgt, d_c, tree)
+        idx, dist = correspondences(moved, tgt, d_c, tree, workers=workers)
         q = np.zeros_like(src)
         q[idx >= 0] = tgt[idx[idx >= 0]]
         W = weights_model(cs, tgt_cov, idx, method, tgt_cnt)

@@ -109,6 +109,22 @@ def test_align_1m_properties(eng, scene1m):
         assert np.array_equal(T, T2), env
 
 
+def test_align_1m_vs_oracle_loop(scene1m):
+    """configs[2] itself (the bench's 1M/1M clouds) through the drop-in's whole outer loop against the
+    oracle's loop, iteration by iteration: 5 fixed iterations from the identity (the first, moving ones;
+    the 30-iteration endpoint is checked against ground truth and switch bit-identity above)."""
+    src, tgt, Tgt = scene1m
+    kw = dict(max_iterations=5, tolerance=0.0, **P3)   # tolerance 0: the rule never fires, 5 iterations
+    out = gicp.gicp(src, tgt, full_output=True, verbose=False, **kw)
+    ref = O.gicp(src, tgt, workers=16, **kw)
+    assert len(out[1]) == len(ref[1]) == 6
+    for k, (Tg, To) in enumerate(zip(out[1], ref[1])):
+        # element-wise (an angle from arccos cannot resolve below ~1.5e-8 rad)
+        err = np.max(np.abs(Tg - To))
+        assert err < 1e-9, (k, err)
+    assert S.rotation_angle_error(out[0], Tgt) < S.rotation_angle_error(np.eye(4), Tgt)
+
+
 def test_align_100k_vs_oracle(eng):
     """configs[1]: the whole outer loop at 100k/100k against the oracle's (exact inner solves both)."""
     src, tgt, Tgt = S.scene_pair_3d(100_000)
