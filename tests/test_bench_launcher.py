@@ -72,3 +72,21 @@ def test_gpus_must_match_world_size():
 def test_gpus_must_be_positive(bad):
     r = _run(["--gpus", bad, "--dry-run"])
     assert r.returncode != 0
+
+
+def test_traffic_comes_only_from_a_profile_of_the_same_command():
+    """roofline.traffic is read from the committed PMC summary whose key (workload, steps, warmup) is the
+    line's own; another command's bytes are refused with the reason."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    wl = "3d_room_1000k_1000k_k20"
+    by, f, per_pass, note = b.measured_traffic(wl, 20, 5)   # the driver's command: profiled
+    assert by and by > 48e6 and f.endswith("pmc_traffic.json") and "--steps 20 --warmup 5" in note
+    d = json.load(open(os.path.join(ROOT, f)))
+    assert (d["workload"], d["steps"], d["warmup"], d["launches"]) == (wl, 20, 5, 205)
+    assert len(per_pass["bytes_by_pass"]) == 20
+    by, f, per_pass, note = b.measured_traffic(wl, 30, 5)   # not profiled: no bytes, and why
+    assert by is None and f is None and "no PMC profile of this command (steps 30, warmup 5)" in note
+    assert b.measured_traffic("2d_segments_1000k", 20, 5)[0] is None
