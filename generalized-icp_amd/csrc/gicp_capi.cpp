@@ -1464,6 +1464,24 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
         const int kEvStride = prm.timing_stride > 0 ? std::min(prm.timing_stride, (int)gicp_ctx::kMaxBatch) : 8;
         const int kEvOffset = std::max(0, prm.timing_offset) % kEvStride;
         c->iter_ms.assign((size_t)std::max(0, prm.max_iterations), -1.f);
+#ifdef GICP_TAIL
+        // diagnostic build: one tail record per iteration (gicp_internal.h kTailWords), dumped raw to
+        // $GICP_TAIL_DUMP.<call> after the loop
+        static unsigned long long* d_tail = nullptr;
+        static size_t tail_cap = 0;
+        static int tail_seq = 0;
+        const char* tail_path = std::getenv("GICP_TAIL_DUMP");
+        const size_t ntail = (size_t)std::max(1, prm.max_iterations) * kTailWords;
+        if (tail_path) {
+            if (ntail > tail_cap) {
+                dalloc(d_tail, ntail);
+                tail_cap = ntail;
+            }
+            std::vector<unsigned long long> init(ntail, 0ull);
+            for (size_t k = 0; k < ntail; k += kTailWords) init[k] = ~0ull;
+            HIPCHK(hipMemcpy(d_tail, init.data(), ntail * 8, hipMemcpyHostToDevice));
+        }
+#endif
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
         // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
         // After convergence the remaining launches of a batch exit at once.
@@ -1476,6 +1494,9 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
                 const int it = enq + b;
                 CorrArgs a = corr_args(c, 0);
                 if (it < c->moving_iters) a.unit_map = c->moving_map;
+#ifdef GICP_TAIL
+                if (tail_path) a.tail = d_tail + (size_t)it * kTailWords;
+#endif
                 if (tk > 0) {   // det(W) of every point, for this iteration's top-k rows (gicp.py:170)
                     a.dbg_det = c->d_dbg_det;
                     a.top_tgt = c->d_top_tgt;
@@ -1529,6 +1550,17 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
         }
         const auto t1 = std::chrono::steady_clock::now();
         c->iter_ms.resize((size_t)std::max(0, std::min(hs.iter, prm.max_iterations)));
+#ifdef GICP_TAIL
+        if (tail_path) {
+            std::vector<unsigned long long> h(ntail);
+            HIPCHK(hipMemcpy(h.data(), d_tail, ntail * 8, hipMemcpyDeviceToHost));
+            const std::string path = std::string(tail_path) + "." + std::to_string(tail_seq++);
+            if (FILE* fp = std::fopen(path.c_str(), "wb")) {
+                std::fwrite(h.data(), 8, h.size(), fp);
+                std::fclose(fp);
+            }
+        }
+#endif
         if (trace && hs.iter > 0) {   // the rows of the iterations executed, in one copy per array
             const int ni = std::min(hs.iter, prm.max_iterations);
             std::vector<double> hist((size_t)ni * HS);

@@ -253,7 +253,13 @@ struct CorrArgs {
     int32_t fuse_solve;
     double* hist;
     PeerArgs peer;            // n > 1: the final workgroup exchanges the statistics with its peers in-kernel
+    // GICP_TAIL diagnostic build: this launch's tail record ([kTailWords] realtime stamps, 100 MHz), else null
+    unsigned long long* tail;
 };
+// GICP_TAIL record of one k_corr launch: [0] first workgroup start (min), [1] last partial stored (max),
+// then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
+// sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done
+constexpr int kTailWords = 16;
 
 constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;

@@ -1369,6 +1369,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         P.t[a] = cs0->T[a * (D + 1) + D];
     }
 
+#ifdef GICP_TAIL
+    unsigned long long tl[kTailWords] = {};
+    if (A.tail && threadIdx.x == 0) atomicMin(A.tail, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#define GICP_TAIL_MARK(k) do { if (A.tail) tl[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GICP_TAIL_MARK(k) do {} while (0)
+#endif
     Stamps S;
     S.start();
 #ifdef GICP_TIMELINE
@@ -2200,6 +2207,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         __hip_atomic_store(&A.partials[(int64_t)unit * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef GICP_TAIL
+    if (A.tail && threadIdx.x == 0) atomicMax(A.tail + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     __syncthreads();
     const int ng = (nunits + kGroupWG - 1) / kGroupWG;
     const int g = unit / kGroupWG;   // the reduction follows the unit, not the launch order
@@ -2210,6 +2220,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        GICP_TAIL_MARK(2);
     }
     __syncthreads();
     if (!s_last) return;
@@ -2263,6 +2274,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             __hip_atomic_store(&A.gpart[(int64_t)g * NSX + t], s_sum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GICP_TAIL_MARK(3);
     __syncthreads();
     if (threadIdx.x == 0) {
         __hip_atomic_store(&A.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2272,6 +2284,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        GICP_TAIL_MARK(4);
     }
     __syncthreads();
     if (!s_last) return;
@@ -2281,6 +2294,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     double hv = 0.0;
     if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     sum_rows(A.gpart, 0, ng, s_sum);
+    GICP_TAIL_MARK(5);
     if (A.peer.n > 1) {   // the sum over ranks, in-kernel
         const uint64_t x0 = (uint64_t)wall_clock64();
         if (!peer_exchange<NSX>(A.peer, s_sum)) {
@@ -2299,8 +2313,17 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             A.state->xchg_n += 1.0;
         }
     }
+    GICP_TAIL_MARK(6);
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
     if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    GICP_TAIL_MARK(7);
+#ifdef GICP_TAIL
+    auto tail_out = [&]() {
+        if (A.tail && threadIdx.x == 0)
+            for (int k = 2; k < kTailWords; ++k) A.tail[k] = tl[k];
+    };
+    if (!fuse) tail_out();
+#endif
     if (!fuse || threadIdx.x >= 64) return;
     // LDS after the reduction scratch: the header image (its `stats` field unused: the statistics are s_sum)
     // and the solve's exchange area
@@ -2311,6 +2334,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     if (threadIdx.x < kStateHeader) reinterpret_cast<double*>(s_hdr)[threadIdx.x] = hv;
     wave_sync();
     solve_update<D>(A.state, s_hdr, s_sum, *s_sl, A.hist);
+    GICP_TAIL_MARK(8);
+#ifdef GICP_TAIL
+    tail_out();
+#endif
 }
 
 // One wave: solve_update on the statistics in the device state (after the multi-GPU all-reduce).

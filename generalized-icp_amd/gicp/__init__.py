@@ -382,30 +382,19 @@ def solve_pose(stats, T_k):
 
 
 def _cg_inner(stats, offset, T_k):
-    """2-D reference inner solve: scipy fmin_cg on the closed-form loss (gicp.py:148-154)."""
-    from scipy.optimize import fmin_cg
-
-    H6, g6, c0, _ = expand_stats(stats, 2)
-    H4 = _L2.T @ H6 @ _L2
-    g4 = _L2.T @ g6
-    th = np.arctan2(T_k[1, 0], T_k[0, 0])
-    zk = np.array([T_k[0, 2], T_k[1, 2], T_k[0, 0], T_k[1, 0]])
-
-    def z(x):
-        return np.array([x[0], x[1], np.cos(x[2]), np.sin(x[2])])
-
-    def f(x):
-        dz = z(x) - zk
-        return c0 - 2.0 * g4 @ dz + dz @ H4 @ dz
-
-    def g(x):
-        dz = z(x) - zk
-        v = -2.0 * g4 + 2.0 * (H4 @ dz)
-        return np.array([v[0], v[1], -np.sin(x[2]) * v[2] + np.cos(x[2]) * v[3]])
-
-    del th
-    out = fmin_cg(f=f, x0=offset, fprime=g, disp=False, full_output=True)
-    return out[0], out[1]
+    """2-D reference inner solve (gicp.py:148-154): fmin_cg's algorithm (SciPy 1.15.3, restated natively in
+    gicp_cg_inner_2d, bit-identical to scipy's own on the same objective: tests/test_cg_native.py) on the
+    closed form of the loss from the pass's 26 statistics.  Returns (xopt, fopt)."""
+    st = np.ascontiguousarray(stats, dtype=np.float64)
+    Tk = np.ascontiguousarray(T_k, dtype=np.float64)
+    x0 = np.ascontiguousarray(offset, dtype=np.float64)
+    if st.shape != (stats_size(2),) or Tk.shape != (3, 3) or x0.shape != (3,):
+        raise ValueError("2-D statistics (26), a 3x3 pose and a 3-vector offset expected")
+    x = np.zeros(3)
+    fopt = C.c_double()
+    check(_lib.load().gicp_cg_inner_2d(dptr(st), dptr(Tk), dptr(x0), dptr(x), C.byref(fopt), None), None,
+          "gicp_cg_inner_2d")
+    return x, fopt.value
 
 
 def _loss_2d(x, s, q, W):

@@ -124,6 +124,7 @@ SIGNATURES = {
     "gicp_get_neighbor_counts": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int32)]),
     "gicp_iterate": (C.c_int, [_VP, _DP, _DP, C.POINTER(Debug)]),
     "gicp_solve_pose": (C.c_int, [C.c_int, _DP, _DP, _DP, _DP]),
+    "gicp_cg_inner_2d": (C.c_int, [_DP, _DP, _DP, _DP, _DP, C.POINTER(C.c_int32)]),
     "gicp_pass_info": (C.c_int, [_VP, _DP]),
     "gicp_top_weights": (C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _DP]),
     "gicp_align": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result)]),
@@ -149,7 +150,7 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _DP, C.c_int, C.c_void_p)
 _lib = None
 
 # the sources gicp_build_info()'s hash covers, in the Makefile's HASH_SRCS order
-HASH_SRCS = ("csrc/gicp_kernels.hip", "csrc/gicp_capi.cpp", "csrc/gicp_solver.cpp", "csrc/gicp_internal.h",
+HASH_SRCS = ("csrc/gicp_kernels.hip", "csrc/gicp_capi.cpp", "csrc/gicp_solver.cpp", "csrc/gicp_cg.cpp", "csrc/gicp_internal.h",
              "csrc/gicp_solver.h", "csrc/gicp_solve_dev.h", "../include/gicp_hip.h")
 
 

@@ -242,6 +242,16 @@ int gicp_top_weights(gicp_ctx* ctx, int k, int64_t* src_out, int64_t* tgt_out, d
  * Pure host code, no GPU needed.  Writes T_out and the minimum. */
 int gicp_solve_pose(int dim, const double* stats, const double* T_k, double* T_out, double* loss_out);
 
+/* 2-D inner solve of gicp.py:148-154 as the reference runs it: scipy.optimize.fmin_cg (SciPy 1.15.3:
+ * Polak-Ribiere+ CG, gtol 1e-5, maxiter 600, Wolfe line search dcsrch then wolfe2, c1 1e-4, c2 0.4),
+ * restated natively (csrc/gicp_cg.cpp), on the closed form of the loss from one pass's 2-D statistics
+ * (gicp_iterate's 26 values at pose T_k, 3x3): minimises over the offset x = (tx, ty, theta) from x0
+ * (gicp.py:151).  Writes xopt[3], *fopt (gicp.py:153-154; may be NULL) and counts[4] = {nfev, ngev,
+ * warnflag, iterations} (may be NULL).  Pure host code, no GPU needed.  Replaces the reference's
+ * fmin_cg call at gicp.py:152 (the fast mode's host inner solve). */
+int gicp_cg_inner_2d(const double* stats, const double* T_k, const double* x0, double* xopt, double* fopt,
+                     int32_t* counts);
+
 /* The whole outer loop (gicp.py:116-167) on the GPU: per iteration the correspondence pass
  * (k_corr), the statistics exchange when sharded, the pose solve + convergence test (k_solve). */
 int gicp_align(gicp_ctx* ctx, const double* T0, const gicp_params* p, double* T_out, gicp_result* res);
