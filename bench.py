@@ -187,6 +187,28 @@ def cpu_baseline(src, tgt, kw, workers, iters=1):
     return iters / dt, setup, dt
 
 
+def setup_exchange(eng, gd, rank, world, exchange, share_gpu):
+    """The statistics exchange of a multi-rank run, agreed by every rank: 'peer' tries the in-kernel peer
+    exchange (gd.init_peer returns the same note on every rank when any rank's export, IPC open or probe
+    failed, with the peer path closed everywhere) and then every rank takes RCCL together; 'rccl' goes
+    straight to RCCL.  Two ranks on one GPU (share_gpu) have no RCCL: a failed peer set-up ends the run.
+    Returns (peer_note, comm_ranks, comm_kind) as the context reports them, after checking that they are
+    what was agreed."""
+    peer_note = None
+    if world > 1:
+        if exchange == "peer":
+            peer_note = gd.init_peer(eng, rank, world)
+        if exchange == "rccl" or peer_note is not None:   # asked for, or the peer probe failed on some rank
+            if share_gpu:
+                raise SystemExit(f"rank {rank}: the peer exchange failed on one GPU: {peer_note}")
+            gd.init_comm(eng, rank, world)
+    comm_ranks, _, comm_kind = eng.comm_ranks()
+    want = "peer" if (exchange == "peer" and peer_note is None) else "rccl"
+    if world > 1 and (comm_ranks != world or comm_kind != want):
+        raise SystemExit(f"rank {rank}: the exchange reports {comm_ranks} ranks ({comm_kind}), expected {world} ({want})")
+    return peer_note, comm_ranks, comm_kind
+
+
 def main():
     a = parse()
     if a.gpus < 1:
@@ -220,18 +242,7 @@ def main():
     src, tgt, Tgt, kw, name = workload(a.n, a.dim)
     params = gicp.default_params(a.dim, fixed_iterations=1, **kw)
     eng = gicp.Engine(dev)
-    peer_note = None
-    if world > 1:
-        if a.exchange == "peer":
-            peer_note = gd.init_peer(eng, rank, world)
-        if a.exchange == "rccl" or peer_note is not None:   # asked for, or the peer probe failed on some rank
-            if a.share_gpu:
-                raise SystemExit(f"rank {rank}: the peer exchange failed on one GPU: {peer_note}")
-            gd.init_comm(eng, rank, world)
-    comm_ranks, _, comm_kind = eng.comm_ranks()
-    want = "peer" if (a.exchange == "peer" and peer_note is None) else "rccl"
-    if world > 1 and (comm_ranks != world or comm_kind != want):
-        raise SystemExit(f"rank {rank}: the exchange reports {comm_ranks} ranks ({comm_kind}), expected {world} ({want})")
+    peer_note, comm_ranks, comm_kind = setup_exchange(eng, gd, rank, world, a.exchange, a.share_gpu)
     t0 = time.perf_counter()
     eng.set_target(tgt, params)
     if world == 1 and a.shard_sim > 1:

@@ -54,16 +54,26 @@ struct Fail {
     std::string msg;
 };
 
+// a failing HIP call is reported to the caller (the exception) and its error cleared from HIP's
+// per-thread last error here, so it cannot fail a later call's first launch check
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \
         hipError_t e_ = (x);                                                                       \
-        if (e_ != hipSuccess) throw Fail{GICP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+        if (e_ != hipSuccess) {                                                                    \
+            (void)hipGetLastError();                                                               \
+            throw Fail{GICP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)};               \
+        }                                                                                          \
     } while (0)
+
+// a HIP call whose failure is deliberately ignored (teardown): its error must not linger either
+inline void quiet(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+}
 
 template <class T>
 void dalloc(T*& p, size_t n) {
     if (p) {
-        (void)hipFree(p);
+        quiet(hipFree(p));
         p = nullptr;
     }
     if (n == 0) n = 1;
@@ -71,7 +81,7 @@ void dalloc(T*& p, size_t n) {
 }
 template <class T>
 void dfree(T*& p) {
-    if (p) (void)hipFree(p);
+    if (p) quiet(hipFree(p));
     p = nullptr;
 }
 // grow-only device buffer: reallocates (contents dropped) only when n exceeds the capacity, with
@@ -268,7 +278,7 @@ struct BuildScratch {
         dfree(g_nb);
         dfree(g_nbh);
         dfree(d_amb);
-        if (h_pinned) (void)hipHostFree(h_pinned);
+        if (h_pinned) quiet(hipHostFree(h_pinned));
         h_pinned = nullptr;
         pool.reset();
         cap_in = cap_codes = cap_codes2 = cap_idx = cap_sort = cap_gnb = cap_gnbh = cap_pinned = 0;
@@ -357,7 +367,7 @@ struct gicp_ctx {
     double* d_peer_area = nullptr;    // this rank's exchange area (uncached device memory, IPC-exported)
     void* peer_open[kMaxPeers] = {};  // the peers' areas as opened here (closed by gicp_peer_close)
     PeerArgs peer{};                  // n > 1 while the peer exchange is on
-    uint64_t peer_seq = 0;            // sequence number of the last exchange launch (the same on every rank)
+    uint64_t* d_peer_ctr = nullptr;   // the device's exchange counter (PeerArgs::ctr)
     double peer_timeout_s = 10.0;
     double* d_probe = nullptr;
     double** d_peer_ptrs = nullptr;   // device copy of the areas' addresses (PeerArgs::area)
@@ -863,10 +873,7 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.gap_slack = (float)std::ldexp(std::sqrt((double)a.search2) + 2.0 * c->tgt.rho + 2.0 * c->src.rho, -19);
     a.cov_model = c->psrc.cov_model;
     a.pl_inv = 1.0 / (c->ptgt.epsilon * (1.0 - c->ptgt.ratio));   // target m = sqrt(eps (1 - ratio)) n
-    if (c->peer.n > 1) {   // every launch is an exchange: ranks count launches alike (same calls, same order)
-        a.peer = c->peer;
-        a.peer.seq = ++c->peer_seq;
-    }
+    if (c->peer.n > 1) a.peer = c->peer;   // (the exchange's sequence number is counted on the device)
     return a;
 }
 
@@ -1063,9 +1070,9 @@ namespace {
 void close_peers(gicp_ctx* c) {
     bool any = c->peer.n > 1;
     for (void* p : c->peer_open) any = any || p != nullptr;
-    if (any) (void)hipStreamSynchronize(c->stream);   // no launch of ours still uses the mappings
+    if (any) quiet(hipStreamSynchronize(c->stream));   // no launch of ours still uses the mappings
     for (auto& p : c->peer_open) {
-        if (p) (void)hipIpcCloseMemHandle(p);
+        if (p) quiet(hipIpcCloseMemHandle(p));
         p = nullptr;
     }
     c->peer = PeerArgs{};
@@ -1074,7 +1081,6 @@ void close_peers(gicp_ctx* c) {
 int guard_impl(gicp_ctx* c, const char* where, const std::function<void()>& body) {
     try {
         if (c) HIPCHK(hipSetDevice(c->device));
-        (void)hipGetLastError();   // a failure an earlier call reported must not fail this call's first launch
         body();
         return GICP_OK;
     } catch (const Fail& f) {
@@ -1153,14 +1159,15 @@ void gicp_destroy(gicp_ctx* c) {
     if (!c) return;
     for (auto& g : c->stg)
         if (g.th.joinable()) g.th.join();        // staged builds still running
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    quiet(hipSetDevice(c->device));
+    if (c->stream) quiet(hipStreamSynchronize(c->stream));
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& p : c->peer_open)
-        if (p) (void)hipIpcCloseMemHandle(p);
-    if (c->d_peer_area) (void)hipFree(c->d_peer_area);
+        if (p) quiet(hipIpcCloseMemHandle(p));
+    if (c->d_peer_area) quiet(hipFree(c->d_peer_area));
     dfree(c->d_probe);
     dfree(c->d_peer_ptrs);
+    dfree(c->d_peer_ctr);
     c->tgt.release();
     c->src.release();
     dfree(c->d_hint);
@@ -1188,18 +1195,18 @@ void gicp_destroy(gicp_ctx* c) {
     for (auto& g : c->stg) {
         g.bs.release();
         g.cl.release();
-        if (g.stream) (void)hipStreamDestroy(g.stream);
+        if (g.stream) quiet(hipStreamDestroy(g.stream));
     }
-    if (c->h_state) (void)hipHostFree(c->h_state);
-    if (c->h_top) (void)hipHostFree(c->h_top);
-    if (c->h_xchg) (void)hipHostFree(c->h_xchg);
+    if (c->h_state) quiet(hipHostFree(c->h_state));
+    if (c->h_top) quiet(hipHostFree(c->h_top));
+    if (c->h_xchg) quiet(hipHostFree(c->h_xchg));
     dfree(c->d_rot);
     dfree(c->d_hist);
     dfree(c->d_trace_top);
     dfree(c->d_trace_det);
     for (auto& e : c->ev)
-        if (e) (void)hipEventDestroy(e);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (e) quiet(hipEventDestroy(e));
+    if (c->stream) quiet(hipStreamDestroy(c->stream));
     delete c;
 }
 
@@ -1756,16 +1763,24 @@ int gicp_set_allreduce_ranks(gicp_ctx* c, gicp_allreduce_fn fn, void* user, int 
 int gicp_peer_export(gicp_ctx* c, char handle[GICP_PEER_HANDLE_BYTES]) {
     if (!c || !handle) return GICP_E_INVALID;
     return guard_impl(c, "gicp_peer_export", [&] {
-        static_assert(sizeof(hipIpcMemHandle_t) == GICP_PEER_HANDLE_BYTES, "IPC handle size");
+        static_assert(sizeof(hipIpcMemHandle_t) + sizeof(uint64_t) == GICP_PEER_HANDLE_BYTES, "IPC handle + counter");
         if (!c->d_peer_area) {   // uncached: peers' stores and this rank's polling meet in memory
             HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->d_peer_area), sizeof(double) * kPeerAreaDoubles,
                                          hipDeviceMallocUncached));
             HIPCHK(hipMemset(c->d_peer_area, 0, sizeof(double) * kPeerAreaDoubles));
             HIPCHK(hipDeviceSynchronize());
         }
+        if (!c->d_peer_ctr) {
+            dalloc(c->d_peer_ctr, 1);
+            HIPCHK(hipMemset(c->d_peer_ctr, 0, sizeof(uint64_t)));
+        }
         hipIpcMemHandle_t h;
         HIPCHK(hipIpcGetMemHandle(&h, c->d_peer_area));
+        uint64_t seq = 0;   // this rank's exchange counter (its launches have finished: stream sync)
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(&seq, c->d_peer_ctr, sizeof(seq), hipMemcpyDeviceToHost));
         std::memcpy(handle, &h, sizeof(h));
+        std::memcpy(handle + sizeof(h), &seq, sizeof(seq));
     });
 }
 
@@ -1773,12 +1788,21 @@ int gicp_peer_init(gicp_ctx* c, int nranks, int rank, const char* handles, doubl
     if (!c || !handles || nranks < 2 || nranks > GICP_MAX_PEERS || rank < 0 || rank >= nranks || !(timeout_s > 0.0))
         return GICP_E_INVALID;
     return guard_impl(c, "gicp_peer_init", [&] {
-        if (!c->d_peer_area) throw Fail{GICP_E_STATE, "gicp_peer_export first"};
+        if (!c->d_peer_area || !c->d_peer_ctr) throw Fail{GICP_E_STATE, "gicp_peer_export first"};
         close_peers(c);
         PeerArgs p{};
         p.n = nranks;
         p.rank = rank;
         p.own = c->d_peer_area;
+        p.ctr = c->d_peer_ctr;
+        // every rank starts at the largest counter any rank exported: above every flag left in any area
+        uint64_t seq0 = 0;
+        for (int r = 0; r < nranks; ++r) {
+            uint64_t v = 0;
+            std::memcpy(&v, handles + (size_t)r * GICP_PEER_HANDLE_BYTES + sizeof(hipIpcMemHandle_t), sizeof(v));
+            seq0 = std::max(seq0, v);
+        }
+        HIPCHK(hipMemcpy(c->d_peer_ctr, &seq0, sizeof(seq0), hipMemcpyHostToDevice));
         double* area[kMaxPeers] = {};
         try {
             for (int r = 0; r < nranks; ++r) {
@@ -1806,7 +1830,6 @@ int gicp_peer_init(gicp_ctx* c, int nranks, int rank, const char* handles, doubl
             p.timeout = (uint64_t)(timeout_s * (khz > 0 ? khz : 100000) * 1e3);
             // the probe: one exchange of (rank + 1, 1), which every rank runs now
             if (!c->d_probe) dalloc(c->d_probe, 2);
-            p.seq = ++c->peer_seq;
             HIPCHK(launch_peer_probe(p, c->d_probe, c->stream));
             double got[2] = {0, 0};
             HIPCHK(hipMemcpyAsync(got, c->d_probe, sizeof(got), hipMemcpyDeviceToHost, c->stream));

@@ -183,9 +183,14 @@ constexpr int kMaxGroups = 4096;   // ticket counters available
 // owns an exchange area in fine-grained (uncached) device memory, mapped into every peer by IPC:
 //   uint64 flag[2][kMaxPeers]              sequence number of the launch whose slot last arrived
 //   double slot[2][kMaxPeers][kPeerSlot]   rank p's statistics of that launch
-// indexed [parity of the launch's sequence number][sending rank].  Two parities suffice: a rank writes
-// launch s + 1's slot only after its launch s read every slot of s (stream order), and launch s + 2's
-// only after every rank wrote s + 1's, i.e. after every rank finished reading s.
+// indexed [parity of the exchange's sequence number][sending rank].  The sequence number counts the
+// exchanges that actually happen (a launch that exits at once after convergence takes none): it is kept on
+// the device (PeerArgs::ctr, the last number this rank wrote flags for) and advanced by the final workgroup
+// as it exchanges, so consecutive exchanges always alternate parity.  Two parities then suffice: a rank
+// writes exchange s + 1's slot only after its exchange s read every slot of s (stream order), and exchange
+// s + 2's only after every rank wrote s + 1's flag, i.e. after every rank finished reading s.  gicp_peer_init
+// starts every rank's counter at the maximum over the ranks (carried in the exported handles), so no flag
+// left in any area by earlier exchanges (a timed-out one included) can pass for a new one.
 constexpr int kMaxPeers = GICP_MAX_PEERS;
 constexpr int kPeerSlot = 80;
 constexpr int kPeerFlagWords = 2 * kMaxPeers;   // doubles before the slots
@@ -195,7 +200,7 @@ struct PeerArgs {
     double* own;               // = area[rank]
     int32_t n;                 // ranks (0: no peer exchange)
     int32_t rank;
-    uint64_t seq;              // this launch's sequence number (>= 1, the same on every rank)
+    uint64_t* ctr;             // device word: the sequence number of this rank's last exchange (flags written)
     uint64_t timeout;          // wall-clock ticks (wall_clock64) a rank waits for its peers
 };
 

@@ -1245,12 +1245,12 @@ constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second h
 // rank.  Returns false on a timeout (uniform over the workgroup).  System-scope stores and a system
 // release before the flags; acquire loads on the flags; the areas are uncached device memory.
 template <int NV>
-__device__ bool peer_exchange(const PeerArgs P, double* vals) {   // (by value: a reference into the kernel
-                                                                  // arguments made them a scratch copy)
+__device__ bool peer_exchange(const PeerArgs P, uint64_t seq, double* vals) {   // (P by value: a reference into
+                                                                             // the kernel arguments made a scratch copy)
     static_assert(NV <= kPeerSlot, "an exchange slot holds the values");
     __shared__ int s_fail;
     const int R = P.n, me = P.rank, tid = (int)threadIdx.x, nt = (int)blockDim.x;
-    const int par = (int)(P.seq & 1u);
+    const int par = (int)(seq & 1u);
     for (int p = 0; p < R; ++p) {   // (p uniform: one scalar load of each peer's pointer)
         double* const dst = P.area[p] + kPeerFlagWords + (size_t)(par * kMaxPeers + me) * kPeerSlot;
         for (int k = tid; k < NV; k += nt) __hip_atomic_store(dst + k, vals[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1260,10 +1260,11 @@ __device__ bool peer_exchange(const PeerArgs P, double* vals) {   // (by value: 
     __syncthreads();          // ... every thread's, before any flag
     if (tid < R) {
         uint64_t* f = reinterpret_cast<uint64_t*>(P.area[tid]) + par * kMaxPeers + me;
-        __hip_atomic_store(f, P.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) *P.ctr = seq;   // flags of `seq` are out (also when the wait below times out)
         const uint64_t* g = reinterpret_cast<const uint64_t*>(P.own) + par * kMaxPeers + tid;
         const uint64_t t0 = (uint64_t)wall_clock64();
-        while (__hip_atomic_load(g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != P.seq) {
+        while (__hip_atomic_load(g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
             if ((uint64_t)wall_clock64() - t0 > P.timeout) {
                 s_fail = 1;
                 break;
@@ -1288,12 +1289,14 @@ __device__ bool peer_exchange(const PeerArgs P, double* vals) {   // (by value: 
 // gicp_peer_init's probe: one exchange of (rank + 1, 1) -> out = (sum, ranks), or (-1, -1) on a timeout
 __global__ void __launch_bounds__(64) k_peer_probe(PeerArgs P, double* out) {
     __shared__ double v[2];
+    __shared__ uint64_t s_seq;
     if (threadIdx.x == 0) {
         v[0] = (double)(P.rank + 1);
         v[1] = 1.0;
+        s_seq = *P.ctr + 1;
     }
     __syncthreads();
-    const bool ok = peer_exchange<2>(P, v);
+    const bool ok = peer_exchange<2>(P, s_seq, v);
     if (threadIdx.x == 0) {
         out[0] = ok ? v[0] : -1.0;
         out[1] = ok ? v[1] : -1.0;
@@ -2291,13 +2294,19 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     // the final workgroup.  With no exchange between ranks it also runs the solve and the pose update
     // (gicp_solve_dev.h, one wave) -- the state header is requested now, in flight with the reduction's loads
     const bool fuse = A.fuse_solve != 0;
+    const bool xchg = A.peer.n > 1;
     double hv = 0.0;
     if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
+    __shared__ uint64_t s_seq;
+    uint64_t seq0 = 0;   // this rank's exchange counter, in flight with the sums' loads
+    if (xchg && threadIdx.x == 0) seq0 = *A.peer.ctr;
     sum_rows(A.gpart, 0, ng, s_sum);
     GICP_TAIL_MARK(5);
-    if (A.peer.n > 1) {   // the sum over ranks, in-kernel
+    if (xchg) {   // the sum over ranks, in-kernel
+        if (threadIdx.x == 0) s_seq = seq0 + 1;
+        __syncthreads();
         const uint64_t x0 = (uint64_t)wall_clock64();
-        if (!peer_exchange<NSX>(A.peer, s_sum)) {
+        if (!peer_exchange<NSX>(A.peer, s_seq, s_sum)) {
             if (threadIdx.x == 0) {   // a peer never arrived: fail the call, later launches exit at once
                 A.state->solve_fail = 2;
                 A.state->converged = 1;

@@ -675,6 +675,11 @@ def _device_loop(engines, src, tgt, T, p, full_output, verbose, init_src_cov, ta
     G = len(engines)
     k = 5 if full_output else 0
     xchg = _ThreadSum(G) if G > 1 else None
+    if xchg is not None:   # installing this call's hook would tear down an RCCL communicator or peer exchange
+        own = [e.comm_ranks()[2] for e in engines]
+        if any(k in ("rccl", "peer") for k in own):
+            raise ValueError(f"gicp(devices=...): the cached engines carry their own statistics exchange ({own}); "
+                             "a multi-device call needs engines without one (close it, or use distributed.align)")
     prev = [e._hook_fn for e in engines]   # a hook the caller installed on the cached engines
     if xchg is not None:
         for r, e in enumerate(engines):

@@ -21,7 +21,7 @@ GICP_E_STATE = -3
 GICP_E_COMM = -4
 GICP_E_NOMEM = -5
 COMM_ID_BYTES = 128
-PEER_HANDLE_BYTES = 64
+PEER_HANDLE_BYTES = 72
 MAX_PEERS = 16
 PASS_INFO = 6
 GRAPH_K = 20

@@ -147,15 +147,20 @@ int gicp_comm_ranks(gicp_ctx* ctx, int* nranks, int* rank, int* kind);
  * exports one small exchange area of its own device memory (fine-grained, uncached) as an IPC handle
  * (gicp_peer_export), the handles are all-gathered out of band, and gicp_peer_init maps the peers' areas.
  * From then on the final workgroup of each correspondence launch writes this rank's statistics into its
- * slot of every rank's area, raises a per-launch sequence number there, waits (bounded by `timeout_s`)
- * until every rank's slot of this launch has arrived in its own area, sums them in rank order -- the same
- * bits on every rank -- and runs the pose solve in the same launch: no collective and no second kernel per
- * iteration.  gicp_peer_init is collective (every rank, same order of calls) and proves the path with one
- * probe exchange before it returns; on GICP_E_COMM the context keeps its previous exchange (RCCL / hook /
- * none).  A timed-out exchange inside gicp_align fails the call with GICP_E_COMM.  `handles` holds
- * nranks x GICP_PEER_HANDLE_BYTES bytes in rank order (this rank's entry is not opened).  Ranks of one GPU
- * (several processes) and of several GPUs (xGMI) use the same protocol.  gicp_comm_ranks reports kind 3. */
-#define GICP_PEER_HANDLE_BYTES 64
+ * slot of every rank's area, raises the exchange's sequence number there, waits (bounded by `timeout_s`)
+ * until every rank's slot of this exchange has arrived in its own area, sums them in rank order -- the
+ * same bits on every rank -- and runs the pose solve in the same launch: no collective and no second kernel
+ * per iteration.  The sequence number counts the exchanges that happen (launches that exit at once after
+ * convergence take none) and lives on the device; an exported handle carries this rank's current number
+ * after the 64-byte IPC handle, and gicp_peer_init starts every rank at the maximum, so the ranks agree
+ * again after a timed-out exchange.  gicp_peer_init is collective (every rank, same order of calls) and
+ * proves the path with one probe exchange before it returns.  It first closes this context's previous peer
+ * exchange; on success it replaces RCCL / the host hook, on failure (GICP_E_COMM) the context is left with
+ * no peer exchange and its RCCL communicator / hook as they were.  A timed-out exchange inside gicp_align
+ * fails the call with GICP_E_COMM.  `handles` holds nranks x GICP_PEER_HANDLE_BYTES bytes in rank order
+ * (this rank's entry is not opened).  Ranks of one GPU (several processes) and of several GPUs (xGMI) use
+ * the same protocol.  gicp_comm_ranks reports kind 3. */
+#define GICP_PEER_HANDLE_BYTES 72
 #define GICP_MAX_PEERS 16
 int gicp_peer_export(gicp_ctx* ctx, char handle[GICP_PEER_HANDLE_BYTES]);
 int gicp_peer_init(gicp_ctx* ctx, int nranks, int rank, const char* handles, double timeout_s);

@@ -92,7 +92,7 @@ def covariances(points, d_n, k=None, epsilon=EPSILON, ratio=RATIO, min_neighbors
     w = valid[..., None].astype(np.float64)
     mean = (nb * w).sum(1) / np.maximum(count, 1)[:, None]
     c = (nb - mean[:, None, :]) * w
-    cov = np.einsum("nki,nkj->nij", c, c) / np.maximum(count - 1, 1)[:, None, None]
+    cov = np.matmul(c.transpose(0, 2, 1), c) / np.maximum(count - 1, 1)[:, None, None]
     if dim == 2:
         ev, evec = np.linalg.eig(cov[ok])
         e = evec[np.arange(ok.sum()), :, np.argmax(ev, axis=1)]
@@ -317,7 +317,7 @@ def inner_gn(s, q, W, idx, T0, max_iter=100, tol=1e-14):
 
     def f(T):
         r = q - s @ T[:d, :d].T - T[:d, d]
-        return np.einsum("na,nab,nb->", r, W, r)
+        return float(np.sum(r * np.matmul(W, r[:, :, None])[:, :, 0]))
 
     if len(s) == 0:
         return T, 0.0
@@ -334,11 +334,15 @@ def inner_gn(s, q, W, idx, T0, max_iter=100, tol=1e-14):
             J[:, :, 1:] = -np.eye(2)
         else:
             J = np.zeros((len(s), 3, 6))          # d r / d(omega, dt)
-            J[:, :, :3] = np.stack([skew(v) for v in p])    # -[w]x p = [p]x w
+            J[:, 0, 1], J[:, 0, 2] = -p[:, 2], p[:, 1]       # -[w]x p = [p]x w (skew(p), row by row)
+            J[:, 1, 0], J[:, 1, 2] = p[:, 2], -p[:, 0]
+            J[:, 2, 0], J[:, 2, 1] = -p[:, 1], p[:, 0]
             J[:, :, 3:] = -np.eye(3)
-        JW = np.einsum("nka,nkb->nab", J, W)
-        Hm = np.einsum("nab,nbc->ac", JW, J)
-        gv = np.einsum("nab,nb->a", JW, r)
+        JW = np.matmul(J.transpose(0, 2, 1), W)                       # J^T W per point
+        na = JW.shape[1]
+        JWf = JW.transpose(1, 0, 2).reshape(na, -1)                  # sums over points as one GEMM each
+        Hm = JWf @ J.reshape(-1, na)
+        gv = JWf @ r.reshape(-1)
         while True:
             step = -np.linalg.solve(Hm + lam * np.diag(np.diag(Hm)), gv)
             Tn = np.eye(d + 1)
@@ -414,7 +418,7 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
             cs, _ = covariances(moved, d_n, k, workers=workers)
         else:
             R = T[:d, :d]
-            cs = np.einsum("ab,nbc,dc->nad", R, init_src_cov, R)
+            cs = np.matmul(np.matmul(R, init_src_cov), R.T)
         all_src_cov.append(cs)
         idx, dist = correspondences(moved, tgt, d_c, tree, workers=workers)
         q = np.zeros_like(src)

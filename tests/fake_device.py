@@ -8,7 +8,7 @@ product still fails loudly when the real library or the GPU is missing.
 
 Every computation is the oracle's (``oracle/gicp_oracle.py``: cKDTree correspondences, the reference's
 covariance rule, the DESIGN.md §4 statistics); the pose solve is the real library's host entry point
-``gicp_solve_pose`` (pure host code, callable without a GPU).  Shards are contiguous point ranges
+``gicp_solve_pose`` and ``gicp_cg_inner_2d`` (pure host code, callable without a GPU).  Shards are contiguous point ranges
 (the real library deals Morton tiles round-robin; only the sum over shards is specified).
 """
 from __future__ import annotations
@@ -60,6 +60,9 @@ class FakeLib:
 
     def gicp_solve_pose(self, *a):
         return self._real.gicp_solve_pose(*a)
+
+    def gicp_cg_inner_2d(self, *a):
+        return self._real.gicp_cg_inner_2d(*a)
 
     def gicp_stats_size(self, dim):
         return O.stats_size(dim)

@@ -90,3 +90,94 @@ def test_traffic_comes_only_from_a_profile_of_the_same_command():
     by, f, per_pass, note = b.measured_traffic(wl, 30, 5)   # not profiled: no bytes, and why
     assert by is None and f is None and "no PMC profile of this command (steps 30, warmup 5)" in note
     assert b.measured_traffic("2d_segments_1000k", 20, 5)[0] is None
+
+
+class _FakeEngine:
+    """The exchange surface of gicp.Engine, no GPU: peer_init fails on the ranks in `fail_on`."""
+
+    def __init__(self, rank, world, fail_on=(), export_fail_on=()):
+        self.rank, self.world, self.kind = rank, world, "none"
+        self.fail_on, self.export_fail_on = set(fail_on), set(export_fail_on)
+        self.calls = []
+
+    def peer_export(self):
+        self.calls.append("export")
+        if self.rank in self.export_fail_on:
+            raise RuntimeError("export failed (fake)")
+        return bytes([self.rank]) * 72
+
+    def peer_init(self, n, r, handles, timeout=10.0):
+        self.calls.append("peer_init")
+        assert len(handles) == n and all(len(h) == 72 for h in handles)
+        if r in self.fail_on:
+            raise RuntimeError("probe failed (fake)")
+        self.kind = "peer"
+
+    def peer_close(self):
+        self.calls.append("peer_close")
+        self.kind = "none"
+
+    def comm_init(self, n, r, uid):
+        self.calls.append("comm_init")
+        assert uid == b"uid" * 4
+        self.kind = "rccl"
+
+    def comm_ranks(self):
+        return (self.world if self.kind != "none" else 1), self.rank, self.kind
+
+
+def _exchange_rank(rank, world, port, d, exchange, fail_on, export_fail_on, share_gpu):
+    import json as js
+    import torch.distributed as dist
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "generalized-icp_amd")]
+    import bench
+    from gicp import distributed as gd
+
+    class _E:   # gd.init_comm's unique id (the real one asks RCCL)
+        @staticmethod
+        def comm_unique_id():
+            return b"uid" * 4
+    gd.Engine = _E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _FakeEngine(rank, world, fail_on, export_fail_on)
+    try:
+        note, n, kind = bench.setup_exchange(eng, gd, rank, world, exchange, share_gpu)
+        out = {"note": note, "n": n, "kind": kind, "calls": eng.calls}
+    except SystemExit as e:
+        out = {"exit": str(e), "calls": eng.calls}
+    with open(os.path.join(d, f"x{rank}.json"), "w") as f:
+        js.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["all_ok", "rank1_probe_fails", "rank0_export_fails", "rccl_asked", "shared_gpu_fails"])
+def test_bench_exchange_decision_is_agreed_by_every_rank(tmp_path, case):
+    """bench.py's exchange set-up (setup_exchange) on two gloo ranks with a fake engine: when the peer
+    exchange fails on ANY rank, every rank reports the same note, closes the peer path and takes RCCL;
+    two ranks sharing one GPU (no RCCL) stop instead."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cfg = {"all_ok": ("peer", (), (), False), "rank1_probe_fails": ("peer", (1,), (), False),
+           "rank0_export_fails": ("peer", (), (0,), False), "rccl_asked": ("rccl", (), (), False),
+           "shared_gpu_fails": ("peer", (1,), (), True)}[case]
+    mp.spawn(_exchange_rank, args=(2, port, str(tmp_path), *cfg), nprocs=2, join=True)
+    r = [json.load(open(tmp_path / f"x{k}.json")) for k in range(2)]
+    if case == "shared_gpu_fails":
+        assert all("peer exchange failed on one GPU" in x["exit"] for x in r)
+        return
+    assert r[0].get("note") == r[1].get("note")
+    assert r[0]["kind"] == r[1]["kind"] == ("peer" if case == "all_ok" else "rccl")
+    assert r[0]["n"] == r[1]["n"] == 2
+    if case == "all_ok":
+        assert r[0]["note"] is None and all("comm_init" not in x["calls"] for x in r)
+    elif case == "rccl_asked":
+        assert r[0]["note"] is None and all(x["calls"] == ["comm_init"] for x in r)
+    else:
+        assert "fake" in r[0]["note"]
+        assert all(x["calls"][-2:] == ["peer_close", "comm_init"] for x in r)

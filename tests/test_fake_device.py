@@ -78,7 +78,9 @@ def test_2d_fast_cg_two_devices(fake):
     one = gicp.gicp(src, tgt, devices=[0], **kw)
     two = gicp.gicp(src, tgt, devices=[0, 1], **kw)
     assert isinstance(one[6], gicp.RotatedCovariances)
-    np.testing.assert_allclose(two[0], one[0], atol=1e-6)
+    # fmin_cg stops inexactly (|grad|_inf <= gtol = 1e-5, gicp.py:152): statistics summed over two shards
+    # round differently from one device's, so the two stopping points differ by ~gtol / curvature
+    np.testing.assert_allclose(two[0], one[0], atol=1e-5)
 
 
 def test_odometry_ring_depths_agree(fake):

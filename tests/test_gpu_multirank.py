@@ -176,3 +176,88 @@ def test_peer_exchange_times_out_instead_of_hanging(tmp_path):
     assert r0["err"] == _lib.GICP_E_COMM        # its peer's third exchange never came: bounded, reported
     assert r0["probe"] == _lib.GICP_E_COMM and r0["kind"] == "none"
     assert r0["after"] == 3
+
+
+def _rank_fallback(rank, world, port, d, mode):
+    """One rank's peer_init fails (`mode` 'bad_handle': rank 1 is handed its own handle as rank 0's, so its
+    IPC open fails; 'skip': rank 1 never calls gicp_peer_init, so rank 0's probe kernel waits and times
+    out).  Both ranks must agree on the failure (gd.init_peer returns the same note on each), both end
+    with no peer exchange, and both then register through the host hook with bit-identical poses.  Then
+    the peer exchange is set up again: the ranks' exchange counters differ after the failed probe (rank 0's
+    advanced), and gicp_peer_init must bring them together (the exported counters' maximum)."""
+    import torch
+    import torch.distributed as dist
+    from gicp import _lib
+    from gicp import distributed as gd
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    src, tgt = np.load(os.path.join(d, "src.npy")), np.load(os.path.join(d, "tgt.npy"))
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=8, **P3)
+    eng = gicp.Engine(0)
+    out = {}
+    real_init = eng.peer_init
+    if rank == 1 and mode == "bad_handle":
+        def bad_init(n, r, handles, timeout=10.0):   # rank 0's slot holds rank 1's own area: the open fails
+            return real_init(n, r, [handles[1]] + list(handles[1:]), timeout=timeout)
+        eng.peer_init = bad_init
+    elif rank == 1 and mode == "skip":
+        def no_init(n, r, handles, timeout=10.0):
+            raise _lib.GicpError(_lib.GICP_E_COMM, "rank 1 skips gicp_peer_init (test)")
+        eng.peer_init = no_init
+    out["note"] = gd.init_peer(eng, rank, world, timeout=2.0)
+    out["kind_after_fail"] = eng.comm_ranks()[2]
+
+    def allreduce(buf):
+        t = torch.from_numpy(buf.copy())
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+    eng.set_allreduce(allreduce, nranks=world, rank=rank)
+    out["kind_hook"] = eng.comm_ranks()[2]
+    eng.set_target(tgt, p)
+    eng.set_source(src, p, shard=rank, nshards=world)
+    out["T_hook"], _ = eng.align(None, p)
+    # the peer exchange again, now on both ranks
+    eng.peer_init = real_init
+    eng.set_allreduce(None)
+    out["note2"] = gd.init_peer(eng, rank, world, timeout=20.0)
+    out["kind_peer"] = eng.comm_ranks()[2]
+    out["T_peer"], res = eng.align(None, p)
+    out["iters_peer"] = int(res["iterations"])
+    np.save(os.path.join(d, f"fb{rank}.npy"), np.array(out, dtype=object), allow_pickle=True)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["bad_handle", "skip"])
+def test_peer_init_failure_is_agreed_and_both_ranks_fall_back(tmp_path, mode):
+    src, tgt, _ = S.scene_pair_3d(20_000)
+    np.save(tmp_path / "src.npy", src)
+    np.save(tmp_path / "tgt.npy", tgt)
+    mp.spawn(_rank_fallback, args=(2, _free_port(), str(tmp_path), mode), nprocs=2, join=True)
+    r = [np.load(tmp_path / f"fb{k}.npy", allow_pickle=True).item() for k in range(2)]
+    assert r[0]["note"] is not None and r[0]["note"] == r[1]["note"], (r[0]["note"], r[1]["note"])
+    if mode == "skip":   # rank 0's probe kernel itself timed out (not an IPC open failure)
+        assert r[0]["note"].startswith("rank 0") and "probe" in r[0]["note"], r[0]["note"]
+    assert r[0]["kind_after_fail"] == r[1]["kind_after_fail"] == "none"
+    assert r[0]["kind_hook"] == r[1]["kind_hook"] == "hook"
+    assert np.array_equal(r[0]["T_hook"], r[1]["T_hook"])
+    assert r[0]["note2"] is None and r[1]["note2"] is None
+    assert r[0]["kind_peer"] == r[1]["kind_peer"] == "peer"
+    assert r[0]["iters_peer"] == r[1]["iters_peer"] == 8
+    assert np.array_equal(r[0]["T_peer"], r[1]["T_peer"])
+    # the same registration through either exchange: the same rank-order sums, the same solve
+    np.testing.assert_allclose(r[0]["T_peer"], r[0]["T_hook"], rtol=0, atol=1e-12)
+
+
+def test_peer_exchange_with_an_empty_shard(tmp_path):
+    """A shard with no source tile (more ranks than chunks: 2k points are one chunk, rank 1 gets none) still
+    takes part in every exchange with one empty workgroup; its zero statistics leave the sums equal to the
+    one-process pass, and both ranks end on the same pose."""
+    r, st1, T1, res1, _ = _run(tmp_path, 2_000, 10, fixed=True, exchange="peer")
+    assert np.array_equal(r[0]["T"], r[1]["T"]) and np.array_equal(r[0]["st"], r[1]["st"])
+    scale = np.maximum(np.abs(st1), 1e-12 * np.abs(st1).max())
+    assert np.max(np.abs(r[0]["st"] - st1) / scale) < 1e-12
+    assert int(r[0]["corr"]) == int(res1["correspondences"])
+    np.testing.assert_allclose(r[0]["T"], T1, rtol=0, atol=1e-12)
