@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--fixed", action="store_true", help="fixed iterations (convergence disabled)")
     ap.add_argument("--tolerance", type=float, default=1e-6)
     ap.add_argument("--sync", action="store_true", help="build each scan when needed (no staged double buffer)")
+    ap.add_argument("--copy", action="store_true",
+                    help="staged scans copied by the library before stage_target returns (the default for callers "
+                         "that refill their buffer); without it the bench, which holds every frame untouched in "
+                         "memory, lends them (GICP_STAGE_BORROW: no copy on the calling thread)")
     a = ap.parse_args()
     from gicp import synthetic as S
     from gicp.odometry import Odometry
@@ -45,7 +49,7 @@ def main():
     import gicp
     p = gicp.default_params(3, max_iterations=a.max_iterations, tolerance=a.tolerance,
                             fixed_iterations=1 if a.fixed else 0, **kw)
-    odo = Odometry(3, params=p)
+    odo = Odometry(3, params=p, borrow=not a.copy)
     # warm-up on the first two frames (library init, allocation), then restart the stream
     odo.step(frames[0][0])
     odo.step(frames[1][0], frames[2][0])
@@ -80,7 +84,11 @@ def main():
         "dtype": "f32-screen+f64",
         "data": f"synthetic spinning LiDAR, {a.beams}x{a.azimuths} rays, C2 room (generated in {gen_s:.1f} s, "
                 f"{'torch/' + dev if xp else 'numpy'})",
-        "pipeline": "synchronous builds" if a.sync else "next scan staged on a second stream during each registration",
+        "pipeline": "synchronous builds" if a.sync else
+        ("coming scans staged on their own streams during the registrations before them, " +
+         ("copied by the library (stage_target copy)" if a.copy else "lent to the library (GICP_STAGE_BORROW)")),
+        "accuracy": "model-limited: per-frame error is the reference's covariance model's (the GPU equals the "
+                    "oracle per frame), see frame_error",
         "config": {"workload": f"c5_lidar_{a.frames}f", "points_per_frame": int(np.mean([len(f[0]) for f in frames])),
                    "trajectory": "0.5 m and 0.5 deg yaw per frame (+-10 %), SURVEY.md 8(d)",
                    "max_iterations": a.max_iterations, "fixed_iterations": bool(a.fixed), **kw},

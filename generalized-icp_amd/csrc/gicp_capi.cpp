@@ -341,14 +341,39 @@ struct gicp_ctx {
     // staged targets (gicp_stage_target / gicp_commit_target): a ring of GICP_MAX_STAGED slots, each
     // built into its own cloud on its own stream by a host thread while the current target is
     // registered; commits take them in staging order
+    // Each slot owns a persistent build thread (started on first use): a thread per staged frame cost
+    // tens of microseconds of the caller's time per frame.  state: 0 idle, 1 build queued or running,
+    // 2 built (rc / err hold the outcome); the caller waits for state != 1 before it takes the slot.
     struct Staged {
         Cloud cl;
         BuildScratch bs;
         hipStream_t stream = nullptr;
         std::thread th;
+        std::mutex m;
+        std::condition_variable cv;
+        int state = 0;
+        bool quit = false;
+        const double* xyz = nullptr;   // the slot's pinned copy, or the caller's buffer (GICP_STAGE_BORROW)
+        int64_t M = 0;
+        int dim = 0;
+        bool graph = false;
+        int device = 0;
         gicp_params p{};
         int rc = GICP_OK;
         std::string err;
+        void wait_idle() {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return state != 1; });
+        }
+        void stop() {
+            if (!th.joinable()) return;
+            {
+                std::lock_guard<std::mutex> g(m);
+                quit = true;
+            }
+            cv.notify_all();
+            th.join();
+        }
     };
     Staged stg[GICP_MAX_STAGED];
     int stg_head = 0, stg_count = 0;
@@ -1157,8 +1182,7 @@ int gicp_create(gicp_ctx** out, int device) {
 
 void gicp_destroy(gicp_ctx* c) {
     if (!c) return;
-    for (auto& g : c->stg)
-        if (g.th.joinable()) g.th.join();        // staged builds still running
+    for (auto& g : c->stg) g.stop();             // staged builds still running finish first
     quiet(hipSetDevice(c->device));
     if (c->stream) quiet(hipStreamSynchronize(c->stream));
     if (c->comm) ncclCommDestroy(c->comm);
@@ -1632,30 +1656,70 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
     });
 }
 
+namespace {
+// the slot's build thread: waits for a queued build, runs it on the slot's stream, reports state 2
+void staged_worker(gicp_ctx::Staged* gp) {
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(gp->m);
+            gp->cv.wait(lk, [&] { return gp->quit || gp->state == 1; });
+            if (gp->state != 1) return;   // quit with nothing queued
+        }
+        int rc = GICP_OK;
+        std::string err;
+        try {
+            HIPCHK(hipSetDevice(gp->device));
+            build_cloud(gp->cl, gp->xyz, gp->M, gp->dim, gp->p, gp->graph, gp->bs, gp->stream, true);
+        } catch (const Fail& f) {
+            rc = f.code;
+            err = f.msg;
+        } catch (const std::bad_alloc&) {
+            rc = GICP_E_NOMEM;
+            err = "out of host memory";
+        } catch (...) {
+            rc = GICP_E_INVALID;
+            err = "unknown error";
+        }
+        {
+            std::lock_guard<std::mutex> g(gp->m);
+            gp->rc = rc;
+            gp->err = err;
+            gp->state = 2;
+        }
+        gp->cv.notify_all();
+    }
+}
+}  // namespace
+
 int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p) {
+    return gicp_stage_target_ex(c, xyz, M, dim, p, 0);
+}
+
+int gicp_stage_target_ex(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gicp_params* p, int flags) {
     if (!c) return GICP_E_INVALID;
     return guard_impl(c, "gicp_stage_target", [&] {
         if (c->stg_count >= GICP_MAX_STAGED)
             throw Fail{GICP_E_STATE, "GICP_MAX_STAGED staged targets are pending (gicp_commit_target or gicp_cancel_stage first)"};
         if (!xyz || M <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
+        if (flags & ~GICP_STAGE_BORROW) throw Fail{GICP_E_INVALID, "unknown gicp_stage_target_ex flags"};
         gicp_ctx::Staged& g = c->stg[(c->stg_head + c->stg_count) % GICP_MAX_STAGED];
-        g.p = resolve(dim, p);
+        g.wait_idle();   // (a slot is only reused after its commit or cancel; a build never runs here)
+        const gicp_params prm = resolve(dim, p);
         if (!g.stream) HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-        const size_t need = (size_t)M * dim;
-        if (need > g.bs.cap_pinned) {   // grow-only pinned staging buffer (allocated here, not in the worker)
-            if (g.bs.h_pinned) HIPCHK(hipHostFree(g.bs.h_pinned));
-            g.bs.h_pinned = nullptr;
-            g.bs.cap_pinned = 0;
-            const size_t cap = need + need / 8;
-            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&g.bs.h_pinned), sizeof(double) * cap));
-            g.bs.cap_pinned = cap;
-        }
-        g.rc = GICP_OK;
-        g.err.clear();
-        // the caller's scan is copied into the slot's pinned buffer before this call returns (the caller
-        // may refill its buffer at once): 16 fixed chunks on the calling thread's tiling pool (a 100k-point
-        // frame, 2.4 MB, in ~0.1 ms instead of one thread's ~0.3 ms)
-        {
+        const double* src = xyz;
+        if (!(flags & GICP_STAGE_BORROW)) {
+            const size_t need = (size_t)M * dim;
+            if (need > g.bs.cap_pinned) {   // grow-only pinned staging buffer (allocated here, not in the worker)
+                if (g.bs.h_pinned) HIPCHK(hipHostFree(g.bs.h_pinned));
+                g.bs.h_pinned = nullptr;
+                g.bs.cap_pinned = 0;
+                const size_t cap = need + need / 8;
+                HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&g.bs.h_pinned), sizeof(double) * cap));
+                g.bs.cap_pinned = cap;
+            }
+            // the caller's scan is copied into the slot's pinned buffer before this call returns (the caller
+            // may refill its buffer at once): 16 fixed chunks on the calling thread's tiling pool (a 100k-point
+            // frame, 2.4 MB, in ~0.06 ms instead of one thread's ~0.3 ms)
             const size_t total = sizeof(double) * need;
             char* dst = reinterpret_cast<char*>(g.bs.h_pinned);
             const char* srcb = reinterpret_cast<const char*>(xyz);
@@ -1664,25 +1728,22 @@ int gicp_stage_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const 
                 const size_t b0 = total * k / kChunks, b1 = total * (k + 1) / kChunks;
                 std::memcpy(dst + b0, srcb + b0, b1 - b0);
             });
+            src = g.bs.h_pinned;
         }
-        const bool graph = c->use_graph && c->use_certs;
-        const int dev = c->device;
-        gicp_ctx::Staged* gp = &g;
-        g.th = std::thread([gp, M, dim, graph, dev] {
-            try {
-                HIPCHK(hipSetDevice(dev));
-                build_cloud(gp->cl, gp->bs.h_pinned, M, dim, gp->p, graph, gp->bs, gp->stream, true);
-            } catch (const Fail& f) {
-                gp->rc = f.code;
-                gp->err = f.msg;
-            } catch (const std::bad_alloc&) {
-                gp->rc = GICP_E_NOMEM;
-                gp->err = "out of host memory";
-            } catch (...) {
-                gp->rc = GICP_E_INVALID;
-                gp->err = "unknown error";
-            }
-        });
+        if (!g.th.joinable()) g.th = std::thread(staged_worker, &g);
+        {
+            std::lock_guard<std::mutex> lk(g.m);
+            g.xyz = src;
+            g.M = M;
+            g.dim = dim;
+            g.graph = c->use_graph && c->use_certs;
+            g.device = c->device;
+            g.p = prm;
+            g.rc = GICP_OK;
+            g.err.clear();
+            g.state = 1;
+        }
+        g.cv.notify_all();
         ++c->stg_count;
     });
 }
@@ -1692,9 +1753,14 @@ int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
     return guard_impl(c, "gicp_commit_target", [&] {
         if (!c->stg_count) throw Fail{GICP_E_STATE, "no staged target (gicp_stage_target first)"};
         gicp_ctx::Staged& g = c->stg[c->stg_head];
-        if (g.th.joinable()) g.th.join();
+        g.wait_idle();
         c->stg_head = (c->stg_head + 1) % GICP_MAX_STAGED;
         --c->stg_count;
+        {
+            std::lock_guard<std::mutex> lk(g.m);
+            g.state = 0;
+            g.xyz = nullptr;
+        }
         if (g.rc != GICP_OK) throw Fail{g.rc, "staged build: " + g.err};
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         // the current target (index + covariances) becomes the source, as robot-visualization.py:250
@@ -1716,8 +1782,12 @@ int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
 
 int gicp_cancel_stage(gicp_ctx* c) {
     if (!c) return GICP_E_INVALID;
-    for (auto& g : c->stg)
-        if (g.th.joinable()) g.th.join();
+    for (auto& g : c->stg) {
+        g.wait_idle();
+        std::lock_guard<std::mutex> lk(g.m);
+        g.state = 0;
+        g.xyz = nullptr;
+    }
     c->stg_head = c->stg_count = 0;
     return GICP_OK;
 }

@@ -113,7 +113,7 @@ class Engine:
         self.dim = None
         self.n_src = self.n_tgt = 0
         self.generation = 0        # bumped whenever the source cloud changes (lazy covariance views)
-        self._staged = []          # (array, params) of the staged targets, oldest first: kept alive until committed
+        self._staged = []          # (shape, params, borrowed array or None) of the staged targets, oldest first
         self._hook = None          # keeps the ctypes callback of set_allreduce alive
         self._hook_fn = None       # (fn, nranks, rank) of that hook, to restore it after a gicp() call
 
@@ -193,15 +193,18 @@ class Engine:
 
     MAX_STAGED = 2   # GICP_MAX_STAGED
 
-    def stage_target(self, pts, params=None):
+    def stage_target(self, pts, params=None, borrow=False):
         """Build `pts` as a coming target on its own stream while the current one is registered
         (gicp_stage_target; up to MAX_STAGED pending); commit_target makes the oldest current.  The
-        library copies `pts` before this call returns: the caller may reuse the array at once."""
+        library copies `pts` before this call returns, so the caller may reuse the array at once --
+        unless borrow=True (GICP_STAGE_BORROW): then the build reads the array itself (no copy on this
+        thread) and the caller must not modify it until commit_target / cancel_stage (this object keeps
+        a reference until then)."""
         a = self._cloud(pts)
         p = params or default_params(a.shape[1])
-        check(self._lib.gicp_stage_target(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p)), self._ctx,
-              "gicp_stage_target")
-        self._staged.append((a.shape, p))
+        check(self._lib.gicp_stage_target_ex(self._ctx, dptr(a), a.shape[0], a.shape[1], C.byref(p),
+                                             _lib.GICP_STAGE_BORROW if borrow else 0), self._ctx, "gicp_stage_target")
+        self._staged.append((a.shape, p, a if borrow else None))
 
     def commit_target(self, shard=0, nshards=1):
         """Wait for the oldest staged target; the current target becomes the source, the staged one the target."""

@@ -22,6 +22,7 @@ GICP_E_COMM = -4
 GICP_E_NOMEM = -5
 COMM_ID_BYTES = 128
 PEER_HANDLE_BYTES = 72
+GICP_STAGE_BORROW = 1
 MAX_PEERS = 16
 PASS_INFO = 6
 GRAPH_K = 20
@@ -131,6 +132,7 @@ SIGNATURES = {
     "gicp_align_trace": (C.c_int, [_VP, _DP, C.POINTER(Params), _DP, C.POINTER(Result), C.POINTER(Trace)]),
     "gicp_reset_cache": (C.c_int, [_VP]),
     "gicp_stage_target": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params)]),
+    "gicp_stage_target_ex": (C.c_int, [_VP, _DP, C.c_int64, C.c_int, C.POINTER(Params), C.c_int]),
     "gicp_commit_target": (C.c_int, [_VP, C.c_int, C.c_int]),
     "gicp_cancel_stage": (C.c_int, [_VP]),
     "gicp_get_graph": (C.c_int, [_VP, C.POINTER(C.c_int64), _DP]),

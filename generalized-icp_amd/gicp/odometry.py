@@ -8,7 +8,8 @@ only the new scan is uploaded, sorted, tiled and given covariances.  Given the c
 threads while the current pair is registered (`gicp_stage_target` / `gicp_commit_target`, up to
 GICP_MAX_STAGED ahead), so setup leaves the critical path (the demo likewise prepares the next scan
 while its worker registers, robot-visualization.py:239-252).  A staged scan is copied by the library
-before stage_target returns, so the caller may refill its buffer at once.  `gicp(prev, cur)` maps the
+before stage_target returns, so the caller may refill its buffer at once (borrow=True skips that copy for
+callers that leave their scans untouched until registered).  `gicp(prev, cur)` maps the
 previous sensor frame into the current one (p_cur = T p_prev), so the sensor pose advances by
 T^-1: `composition='se3'` (default) is that exact SE(d) update; `composition='reference'` is the
 demo's first-order update (robot-visualization.py:257-265: translation -T[:2, d], yaw
@@ -23,7 +24,8 @@ from . import Engine, default_params
 
 
 class Odometry:
-    def __init__(self, dim=3, params=None, device=0, composition="se3", init="constant_velocity", **kw):
+    def __init__(self, dim=3, params=None, device=0, composition="se3", init="constant_velocity", borrow=False,
+                 **kw):
         if composition not in ("se3", "reference"):
             raise ValueError("composition must be 'se3' or 'reference'")
         if init not in ("identity", "constant_velocity"):
@@ -33,6 +35,9 @@ class Odometry:
         self.eng = Engine(device)
         self.composition = composition
         self.init = init
+        # borrow=True: staged scans are read by the library in place (GICP_STAGE_BORROW, no copy on this
+        # thread); the caller must not modify a scan passed as a coming scan until it has been step()ped
+        self.borrow = bool(borrow)
         self.reset()
 
     def reset(self):
@@ -79,7 +84,7 @@ class Odometry:
             self.eng.cancel_stage()
             self._staged = []
         for s in want[len(self._staged):]:
-            self.eng.stage_target(self._prep(s), self.params)
+            self.eng.stage_target(self._prep(s), self.params, borrow=self.borrow)
             self._staged.append(s)
         t1 = time.perf_counter()
         self.timing["setup_s"] += t1 - t0

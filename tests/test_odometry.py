@@ -204,3 +204,24 @@ def test_staged_scan_buffer_may_be_refilled_at_once():
         a.close()
         b.close()
     assert np.array_equal(Ta, Tb) and ra["iterations"] == rb["iterations"]
+
+
+@pytest.mark.gpu
+def test_borrowed_staging_equals_copied_staging():
+    """GICP_STAGE_BORROW (no copy: the build reads the caller's buffer in place, the caller leaves it alone
+    until the commit) registers exactly what the copying stage does, through a whole staged stream; the
+    persistent per-slot build threads serve both."""
+    from gicp.odometry import Odometry
+    kw = dict(max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    scans = [s for s, _ in S.lidar_stream(6)]
+    out = {}
+    for borrow in (False, True):
+        import gicp
+        odo = Odometry(3, params=gicp.default_params(3, max_iterations=30, tolerance=1e-9, **kw), borrow=borrow)
+        try:
+            out[borrow] = [(T, r["iterations"]) for T, r in odo.run(scans) if T is not None]
+        finally:
+            odo.eng.close()
+    assert len(out[True]) == len(out[False]) == 5
+    for (Ta, ia), (Tb, ib) in zip(out[False], out[True]):
+        assert np.array_equal(Ta, Tb) and ia == ib
