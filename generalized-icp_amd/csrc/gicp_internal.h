@@ -263,7 +263,9 @@ struct CorrArgs {
 };
 // GICP_TAIL record of one k_corr launch: [0] first workgroup start (min), [1] last partial stored (max),
 // then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
-// sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done
+// sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] why lanes walked
+// (counts, k_corr: no last match / descent local minimum without proof / uncovered near tie / hops exhausted /
+// walking lanes / walking waves / waves with one walking lane)
 constexpr int kTailWords = 16;
 
 constexpr int nstat(int D) {

@@ -1503,6 +1503,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // certificate: every other target is >= min(runner-up, r(j) - d(p', j)) - e away.
         bool gcert = false;
         float ggap = 0.f;
+#ifdef GICP_TAIL
+        int gwhy = 0;   // diagnostic: how the descent ended for a lane it did not prove
+#define GICP_WHY(k) (gwhy = (k))
+#else
+#define GICP_WHY(k) ((void)0)
+#endif
         if (tg.nbq && wave_any(have_jp)) {
             bool act = have_jp;
             int node = jp;
@@ -1608,6 +1614,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         tfar = r - d0 - e;   // every target outside the row is at least this far
                         tnode = node;
                         act = false;                              // else the walk decides
+                        if (!tie) GICP_WHY(2);
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
@@ -1615,6 +1622,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         act = false;
                     } else if (bk < 0) {
                         act = false;                              // local minimum without proof
+                        GICP_WHY(1);
                     } else {                                      // hop: p' relative to the nearer candidate
                         qr[0] = bx;
                         qr[1] = by;
@@ -1624,6 +1632,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     }
                 }
             }
+            if (act) GICP_WHY(3);   // hops exhausted
             // near ties: every candidate of the tie node's row (and the node) exactly in fp64, the nearest
             // by the KD-tree's tie rule (smaller original index); the lane's certificate gap is the exact
             // runner-up among them, or the row's reach when that is nearer
@@ -1676,6 +1685,21 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         const bool any_gcert = wave_any(gcert);
         const bool skip_walk = !wave_any(q.valid && !cert);
+#ifdef GICP_TAIL
+        if (A.tail) {   // why lanes walk: [9] no last match, [10] descent at a local minimum without proof,
+                        // [11] a near tie the row does not cover, [12] hops exhausted, [13] walking lanes,
+                        // [14] walking waves, [15] walking waves with one walking lane
+            const bool wl = q.valid && !cert;
+            const int why = !wl ? -1 : (jp < 0 ? 9 : (gwhy ? 9 + gwhy : 13));
+            const uint64_t wm = __ballot(wl);
+            if (why >= 9 && why <= 12) atomicAdd(A.tail + why, 1ull);
+            if (l == 0 && wm) {
+                atomicAdd(A.tail + 13, (unsigned long long)__popcll(wm));
+                atomicAdd(A.tail + 14, 1ull);
+                if (__popcll(wm) == 1) atomicAdd(A.tail + 15, 1ull);
+            }
+        }
+#endif
         ngproved = __popcll(__ballot(gcert));
         nwalked = skip_walk ? 0 : 1;
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
@@ -2329,7 +2353,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #ifdef GICP_TAIL
     auto tail_out = [&]() {
         if (A.tail && threadIdx.x == 0)
-            for (int k = 2; k < kTailWords; ++k) A.tail[k] = tl[k];
+            for (int k = 2; k < 9; ++k) A.tail[k] = tl[k];
     };
     if (!fuse) tail_out();
 #endif
