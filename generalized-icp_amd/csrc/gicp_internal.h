@@ -171,6 +171,9 @@ struct IterState {
 };
 
 constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
+// grids of at most this many units reduce in one level: the final workgroup sums every unit's partial itself
+// (its loads cover 81 units per round trip, k_corr sum_rows), one ticket and one round trip of stores fewer
+constexpr int kFlatUnits = 243;
 // Source shards are interleaved in chunks of kShardChunk units (a unit = kCorrWaves source tiles,
 // one k_corr workgroup): rank r of G reduces global chunks r, r + G, r + 2G, ...  Contiguous Morton
 // ranges left the ranks unbalanced (the registration's far walls are the heavy tiles: one rank of 8
@@ -261,7 +264,7 @@ struct CorrArgs {
     // GICP_TAIL diagnostic build: this launch's tail record ([kTailWords] realtime stamps, 100 MHz), else null
     unsigned long long* tail;
 };
-// GICP_TAIL record of one k_corr launch: [0] first workgroup start (min), [1] last partial stored (max),
+// GICP_TAIL record of one k_corr launch: [0] workgroup 0's start, [1] the final workgroup's partial stored,
 // then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
 // sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] why lanes walked
 // (counts, k_corr: no last match / descent local minimum without proof / uncovered near tie / hops exhausted /

@@ -1374,7 +1374,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
 #ifdef GICP_TAIL
     unsigned long long tl[kTailWords] = {};
-    if (A.tail && threadIdx.x == 0) atomicMin(A.tail, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    __shared__ unsigned s_walk[8];
+    if (threadIdx.x < 8) s_walk[threadIdx.x] = 0;
+    __syncthreads();
+    if (A.tail && blockIdx.x == 0 && threadIdx.x == 0) A.tail[0] = __builtin_amdgcn_s_memrealtime();   // (first dispatched)
 #define GICP_TAIL_MARK(k) do { if (A.tail) tl[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define GICP_TAIL_MARK(k) do {} while (0)
@@ -1688,15 +1691,19 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #ifdef GICP_TAIL
         if (A.tail) {   // why lanes walk: [9] no last match, [10] descent at a local minimum without proof,
                         // [11] a near tie the row does not cover, [12] hops exhausted, [13] walking lanes,
-                        // [14] walking waves, [15] walking waves with one walking lane
+                        // [14] walking waves, [15] walking waves with one walking lane (per-wave counts into the
+                        // workgroup's LDS, one global add per workgroup at its end)
             const bool wl = q.valid && !cert;
-            const int why = !wl ? -1 : (jp < 0 ? 9 : (gwhy ? 9 + gwhy : 13));
+            const int why = !wl ? -1 : (jp < 0 ? 0 : (gwhy ? gwhy : -1));
             const uint64_t wm = __ballot(wl);
-            if (why >= 9 && why <= 12) atomicAdd(A.tail + why, 1ull);
+            for (int k = 0; k < 4; ++k) {
+                const int c = __popcll(__ballot(why == k));
+                if (l == 0 && c) atomicAdd(&s_walk[k], (unsigned)c);
+            }
             if (l == 0 && wm) {
-                atomicAdd(A.tail + 13, (unsigned long long)__popcll(wm));
-                atomicAdd(A.tail + 14, 1ull);
-                if (__popcll(wm) == 1) atomicAdd(A.tail + 15, 1ull);
+                atomicAdd(&s_walk[4], (unsigned)__popcll(wm));
+                atomicAdd(&s_walk[5], 1u);
+                if (__popcll(wm) == 1) atomicAdd(&s_walk[6], 1u);
             }
         }
 #endif
@@ -2234,15 +2241,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         __hip_atomic_store(&A.partials[(int64_t)unit * NSX + t], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GICP_TAIL_MARK(1);
 #ifdef GICP_TAIL
-    if (A.tail && threadIdx.x == 0) atomicMax(A.tail + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (A.tail && threadIdx.x < 7 && s_walk[threadIdx.x]) atomicAdd(A.tail + 9 + threadIdx.x, (unsigned long long)s_walk[threadIdx.x]);
 #endif
     __syncthreads();
-    const int ng = (nunits + kGroupWG - 1) / kGroupWG;
-    const int g = unit / kGroupWG;   // the reduction follows the unit, not the launch order
+    // one level when a few round trips of the final workgroup's loads cover every unit (kFlatUnits), else
+    // groups of kGroupWG units first
+    const bool flat = nunits <= kFlatUnits;
+    const int ng = flat ? 1 : (nunits + kGroupWG - 1) / kGroupWG;
+    const int g = flat ? 0 : unit / kGroupWG;   // the reduction follows the unit, not the launch order
     if (threadIdx.x == 0) {
-        const int gn = min(kGroupWG, nunits - g * kGroupWG);
-        s_last = __hip_atomic_fetch_add(&A.tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
+        const int gn = flat ? nunits : min(kGroupWG, nunits - g * kGroupWG);
+        uint32_t* const tk = flat ? &A.tickets[kMaxGroups] : &A.tickets[g];
+        s_last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
         if (s_last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2294,37 +2306,41 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         __syncthreads();
     };
-    {
-        const int b0 = g * kGroupWG, b1 = min(nunits, b0 + kGroupWG);
-        sum_rows(A.partials, b0, b1, s_sum);
-        for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves)
-            __hip_atomic_store(&A.gpart[(int64_t)g * NSX + t], s_sum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    GICP_TAIL_MARK(3);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&A.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = __hip_atomic_fetch_add(&A.tickets[kMaxGroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)(ng - 1);
-        if (s_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        GICP_TAIL_MARK(4);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // the final workgroup.  With no exchange between ranks it also runs the solve and the pose update
-    // (gicp_solve_dev.h, one wave) -- the state header is requested now, in flight with the reduction's loads
     const bool fuse = A.fuse_solve != 0;
     const bool xchg = A.peer.n > 1;
     double hv = 0.0;
-    if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     __shared__ uint64_t s_seq;
-    uint64_t seq0 = 0;   // this rank's exchange counter, in flight with the sums' loads
+    uint64_t seq0 = 0;
+    if (!flat) {
+        {
+            const int b0 = g * kGroupWG, b1 = min(nunits, b0 + kGroupWG);
+            sum_rows(A.partials, b0, b1, s_sum);
+            for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves)
+                __hip_atomic_store(&A.gpart[(int64_t)g * NSX + t], s_sum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        GICP_TAIL_MARK(3);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&A.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = __hip_atomic_fetch_add(&A.tickets[kMaxGroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (unsigned)(ng - 1);
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            GICP_TAIL_MARK(4);
+        }
+        __syncthreads();
+        if (!s_last) return;
+    }
+    // the final workgroup.  With no exchange between ranks it also runs the solve and the pose update
+    // (gicp_solve_dev.h, one wave) -- the state header is requested now, in flight with the reduction's loads,
+    // and so is this rank's exchange counter
+    if (fuse && threadIdx.x < kStateHeader) hv = reinterpret_cast<const double*>(A.state)[threadIdx.x];
     if (xchg && threadIdx.x == 0) seq0 = *A.peer.ctr;
-    sum_rows(A.gpart, 0, ng, s_sum);
+    if (flat) sum_rows(A.partials, 0, nunits, s_sum);   // every unit's partial, in unit order
+    else sum_rows(A.gpart, 0, ng, s_sum);
     GICP_TAIL_MARK(5);
     if (xchg) {   // the sum over ranks, in-kernel
         if (threadIdx.x == 0) s_seq = seq0 + 1;
@@ -2353,7 +2369,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #ifdef GICP_TAIL
     auto tail_out = [&]() {
         if (A.tail && threadIdx.x == 0)
-            for (int k = 2; k < 9; ++k) A.tail[k] = tl[k];
+            for (int k = 1; k < 9; ++k) A.tail[k] = tl[k];
     };
     if (!fuse) tail_out();
 #endif
