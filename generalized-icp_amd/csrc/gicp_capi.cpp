@@ -837,8 +837,8 @@ void ensure_workspace(gicp_ctx* c) {
         dalloc(c->d_state, 1);
         HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->h_state), sizeof(IterState)));
         std::memset(c->h_state, 0, sizeof(IterState));
-        dalloc(c->d_tickets, kMaxGroups + 1);
-        HIPCHK(hipMemsetAsync(c->d_tickets, 0, sizeof(uint32_t) * (kMaxGroups + 1), c->stream));
+        dalloc(c->d_tickets, (size_t)(kMaxGroups + 1) * kTicketStride);
+        HIPCHK(hipMemsetAsync(c->d_tickets, 0, sizeof(uint32_t) * (kMaxGroups + 1) * kTicketStride, c->stream));
         dalloc(c->d_gpart, (size_t)kMaxGroups * nsx);
     }
 }

@@ -172,8 +172,9 @@ struct IterState {
 
 constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
 // grids of at most this many units reduce in one level: the final workgroup sums every unit's partial itself
-// (its loads cover 81 units per round trip, k_corr sum_rows), one ticket and one round trip of stores fewer
-constexpr int kFlatUnits = 243;
+// (its loads cover 81 units per round trip, k_corr sum_rows), one ticket and one round trip of stores fewer;
+// beyond it the one ticket's queue (every unit on one counter) and a third round trip of loads cost more
+constexpr int kFlatUnits = 128;
 // Source shards are interleaved in chunks of kShardChunk units (a unit = kCorrWaves source tiles,
 // one k_corr workgroup): rank r of G reduces global chunks r, r + G, r + 2G, ...  Contiguous Morton
 // ranges left the ranks unbalanced (the registration's far walls are the heavy tiles: one rank of 8
@@ -181,6 +182,9 @@ constexpr int kFlatUnits = 243;
 // of 64 tiles is still one compact region, so an XCD's L2 keeps its locality.
 constexpr int kShardChunk = 16;
 constexpr int kMaxGroups = 4096;   // ticket counters available
+// one 128-B line per ticket counter: agent-scope atomics on one line serialise at the memory side, so tickets
+// sharing a line made the groups' last arrivers queue behind each other (625 units: 2.8 us for the group ticket)
+constexpr int kTicketStride = 32;
 
 // In-kernel peer exchange of the statistics (include/gicp_hip.h gicp_peer_init).  Each rank
 // owns an exchange area in fine-grained (uncached) device memory, mapped into every peer by IPC:
@@ -217,7 +221,8 @@ struct CorrArgs {
     // units dealt round-robin to the XCDs (1 = identity)
     int32_t unit_map;
     IterState* state;         // pose in, statistics out
-    uint32_t* tickets;        // [kMaxGroups + 1] arrival counters, zero between launches (self-resetting)
+    uint32_t* tickets;        // [(kMaxGroups + 1) kTicketStride] arrival counters (one per line), zero between
+                              // launches (self-resetting)
     double* gpart;            // [kMaxGroups][nstat_ext] group partials
     int32_t single_pass;      // 1: run even if state->converged (gicp_iterate)
     float search2;            // fp32 screen bound (d_c^2 + margins)

@@ -2253,7 +2253,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     const int g = flat ? 0 : unit / kGroupWG;   // the reduction follows the unit, not the launch order
     if (threadIdx.x == 0) {
         const int gn = flat ? nunits : min(kGroupWG, nunits - g * kGroupWG);
-        uint32_t* const tk = flat ? &A.tickets[kMaxGroups] : &A.tickets[g];
+        uint32_t* const tk = flat ? &A.tickets[kMaxGroups * kTicketStride] : &A.tickets[g * kTicketStride];
         s_last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(gn - 1);
         if (s_last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2322,8 +2322,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         GICP_TAIL_MARK(3);
         __syncthreads();
         if (threadIdx.x == 0) {
-            __hip_atomic_store(&A.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = __hip_atomic_fetch_add(&A.tickets[kMaxGroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            __hip_atomic_store(&A.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = __hip_atomic_fetch_add(&A.tickets[kMaxGroups * kTicketStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                      (unsigned)(ng - 1);
             if (s_last) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2350,7 +2350,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (threadIdx.x == 0) {   // a peer never arrived: fail the call, later launches exit at once
                 A.state->solve_fail = 2;
                 A.state->converged = 1;
-                __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&A.tickets[kMaxGroups * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             return;
         }
@@ -2364,7 +2364,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     }
     GICP_TAIL_MARK(6);
     for (int t = threadIdx.x; t < NSX; t += 64 * kCorrWaves) A.state->stats[t] = s_sum[t];
-    if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(&A.tickets[kMaxGroups * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     GICP_TAIL_MARK(7);
 #ifdef GICP_TAIL
     auto tail_out = [&]() {

@@ -31,6 +31,27 @@ __global__ void k_ticket(unsigned* t, double* out) {   // last arriver of all wo
     }
 }
 
+// in-kernel latency (100 MHz realtime ticks) of a kernel-argument load and of a device-memory load that the
+// previous launch wrote: where does k_corr's first round trip go
+__global__ void k_lat(Big b, double* dev, unsigned long long* out) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    double v = b.v[80];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" ::"s"(v));
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const double w = __hip_atomic_load(dev + 8 * blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    const double x = dev[4096 + 8 * blockIdx.x];   // plain load
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    dev[8 * blockIdx.x] = v + w + x;   // the next launch reads what this one wrote
+    out[blockIdx.x * 4 + 0] = t1 - t0;
+    out[blockIdx.x * 4 + 1] = t2 - t1;
+    out[blockIdx.x * 4 + 2] = t3 - t2;
+}
+
 template <class F>
 float period(F launch, int n) {
     hipEvent_t a, b;
@@ -66,5 +87,18 @@ int main() {
     printf("1 KB write, 1536 WG    : %.2f us\n", period([&] { hipLaunchKernelGGL(k_write, dim3(1536), dim3(256), 0, 0, d_buf); }, n));
     printf("ticket, 79 WG          : %.2f us\n", period([&] { hipLaunchKernelGGL(k_ticket, dim3(79), dim3(256), 0, 0, d_t, (double*)d_buf); }, n));
     printf("ticket, 625 WG         : %.2f us\n", period([&] { hipLaunchKernelGGL(k_ticket, dim3(625), dim3(256), 0, 0, d_t, (double*)d_buf); }, n));
+    unsigned long long* d_lat;
+    CK(hipMalloc(&d_lat, 64 * 4 * 8));
+    double acc[3] = {0, 0, 0};
+    const int reps = 200;
+    for (int r = 0; r < reps; ++r) {
+        hipLaunchKernelGGL(k_lat, dim3(64), dim3(64), 0, 0, b, (double*)d_buf, d_lat);
+        unsigned long long h[64 * 4];
+        CK(hipMemcpy(h, d_lat, sizeof h, hipMemcpyDeviceToHost));
+        for (int w = 0; w < 64; ++w)
+            for (int k = 0; k < 3; ++k) acc[k] += h[w * 4 + k] / 100.0 / 64 / reps;
+    }
+    printf("in-kernel latency (us): kernarg load %.2f, agent-scope load of data the previous launch wrote %.2f, plain load %.2f\n",
+           acc[0], acc[1], acc[2]);
     return 0;
 }
