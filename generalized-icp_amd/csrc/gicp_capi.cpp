@@ -335,6 +335,7 @@ struct gicp_ctx {
     int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
+    double kappa_far_frac = 0.04;     // ... for lanes the graph could not prove (GICP_CERT_KAPPA_FAR)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
     BuildScratch bs;
@@ -876,6 +877,7 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc + kappa);
     a.search2 = screen_bound(a.mg, dc + kappa);
     a.kappa = (float)kappa;
+    a.kappa_far = (float)std::min(std::max(kappa, c->use_certs ? c->kappa_far_frac * dc : 0.0), dc);
     a.empty_r = (float)dc * (1.0f + 1e-6f);
     if (c->use_certs) {
         a.cert_j = c->d_cert_j;
@@ -1159,6 +1161,7 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
+    if (const char* e = std::getenv("GICP_CERT_KAPPA_FAR")) c->kappa_far_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;

@@ -259,6 +259,7 @@ struct CorrArgs {
     float* cert_gap;          // [src.n] runner-up gap (found) or empty radius R (none), relative to cert_pass
     int32_t* cert_pass;       // [src.ntiles] pass the tile's certificates refer to (-1: none)
     float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
+    float kappa_far;          // ... for lanes the graph descent left at an unproved local minimum (<= kappa: off)
     float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected
     unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
     // 1: the final workgroup also runs the inner solve + pose update (what k_solve does), when no exchange

@@ -1506,6 +1506,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // certificate: every other target is >= min(runner-up, r(j) - d(p', j)) - e away.
         bool gcert = false;
         float ggap = 0.f;
+        bool lmin = false;   // the descent ended at a local minimum it could not prove (a point far from the surface)
 #ifdef GICP_TAIL
         int gwhy = 0;   // diagnostic: how the descent ended for a lane it did not prove
 #define GICP_WHY(k) (gwhy = (k))
@@ -1625,6 +1626,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         act = false;
                     } else if (bk < 0) {
                         act = false;                              // local minimum without proof
+                        lmin = true;
                         GICP_WHY(1);
                     } else {                                      // hop: p' relative to the nearer candidate
                         qr[0] = bx;
@@ -1711,7 +1713,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         nwalked = skip_walk ? 0 : 1;
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
         // farther than kappa since its last pass (the pose is still converging) walks without it
-        const float kap = cdelta > A.kappa ? 0.f : A.kappa;
+        // A lane the descent could not prove at a local minimum (its nearest target is too far for the
+        // graph row's radius) walks, and its runner-up gap is resolved only up to the widening: with kappa
+        // its certificate would break again after a displacement of kappa / 2, and the lane would walk in
+        // pass after pass.  Such lanes widen by kappa_far instead, so their certificate outlasts the settling.
+        const float kw = lmin ? A.kappa_far : A.kappa;
+        const float kap = cdelta > kw ? 0.f : kw;
 
         // ---- fp32 screen: best and runner-up keys -------------------------
         const unsigned init = __float_as_uint(A.search2) | 63u;
