@@ -11,6 +11,7 @@ timeout -k 10 300 python3 bench.py --shard-sim 8 --no-cpu-baseline > $OUT/sim8.j
 timeout -k 10 300 python3 bench.py --n 20000 --shard-sim 2 --steps 100 --no-cpu-baseline > $OUT/sim2_20k.json 2> $OUT/sim2_20k.err || { echo sim2 failed; tail $OUT/sim2_20k.err; exit 1; }
 for f in bench20 c2 sim8 sim2_20k; do python -c "import json;d=json.load(open('$OUT/$f.json'));print('$f',round(d['value'],1),d['unit'],'corr_ms',round(d['roofline']['kernel_avg_ms'],4), 'mov',round(d['passes']['moving_pass_us'],1), 'conv',round(d['passes']['converged_pass_us'],1))"; done
 fi
+[ "${SKIP_TAIL:-0}" = 1 ] && exit 0
 V=${TAIL_VARIANT:-tail}
 GICP_LIB_VARIANT=$V timeout -k 10 200 python3 scripts/tail_run.py --n 1000000 > $OUT/tail_1m.txt 2>&1 || { echo tail1m failed; tail $OUT/tail_1m.txt; exit 1; }
 GICP_LIB_VARIANT=$V timeout -k 10 200 python3 scripts/tail_run.py --n 1000000 --shard-sim 8 > $OUT/tail_sim8.txt 2>&1 || { echo tailsim8 failed; tail $OUT/tail_sim8.txt; exit 1; }
