@@ -94,6 +94,11 @@ struct DevCloud {
     // entry k (-1 unused).
     const uint4* nbq;         // [n][8]
     const int32_t* nbi;       // [n][kGraphK]
+    // target-side tile lists (target only; null when not built), DESIGN.md §3f: tl_list[S][kListMax] the target
+    // tiles near tile S nearest first, tl_len[S] how many, tl_r[S] the box gap below which every tile is listed
+    const int32_t* tl_list;
+    const int32_t* tl_len;
+    const float* tl_r;
     int64_t n;
     int32_t ntiles;
     int32_t nblocks;

@@ -124,6 +124,11 @@ class FakeLib:
         c.staged.append(self._cloud(ptr, n, dim, p))
         return OK
 
+    def gicp_stage_target_ex(self, ctx, ptr, n, dim, p, flags):   # the copy (flags 0) and borrow are alike here
+        if flags & ~1:
+            return self._fail(self._c(ctx), E_INVALID, "unknown gicp_stage_target_ex flags")
+        return self.gicp_stage_target(ctx, ptr, n, dim, p)
+
     def gicp_commit_target(self, ctx, shard, nshards):
         c = self._c(ctx)
         if not c.staged:
