@@ -279,8 +279,9 @@ struct CorrArgs {
 // then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
 // sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] why lanes walked
 // (counts, k_corr: no last match / descent local minimum without proof / uncovered near tie / hops exhausted /
-// walking lanes / walking waves / waves with one walking lane)
-constexpr int kTailWords = 16;
+// walking lanes / walking waves / waves with one walking lane); [16] waves that scanned a target-side list,
+// [17] of which it certified (the tile adopted it)
+constexpr int kTailWords = 20;
 
 constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;

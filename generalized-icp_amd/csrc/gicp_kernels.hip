@@ -1487,8 +1487,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
 #ifdef GICP_TAIL
     unsigned long long tl[kTailWords] = {};
-    __shared__ unsigned s_walk[8];
-    if (threadIdx.x < 8) s_walk[threadIdx.x] = 0;
+    __shared__ unsigned s_walk[9];
+    if (threadIdx.x < 9) s_walk[threadIdx.x] = 0;
     __syncthreads();
     if (A.tail && blockIdx.x == 0 && threadIdx.x == 0) A.tail[0] = __builtin_amdgcn_s_memrealtime();   // (first dispatched)
 #define GICP_TAIL_MARK(k) do { if (A.tail) tl[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -1953,6 +1953,17 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 est = tg.tiles[ent].start;
                 ecnt = tg.tiles[ent].count;
             }
+#ifdef GICP_TAIL
+            if (from_t && A.tail && l == 0) atomicAdd(&s_walk[7], 1u);
+#endif
+            if (from_t) {   // the seed's list is ordered from S's box: reorder it nearest-first to this wave's box,
+                            // so the scan's bound falls fast (and the list this tile adopts is ordered for it)
+                int src = l;
+                wave_sort64(eg2, src);
+                ent = __shfl(ent, src);
+                est = __shfl(est, src);
+                ecnt = __shfl(ecnt, src);
+            }
             float wb = wave_maxf(lb);
             uint64_t rem = __ballot(l < nl && eg2 <= wb);
             // nearest remaining entry (wave-uniform lane index), -1 if none
@@ -1988,6 +1999,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 lbx = inflate(lb);
                 ++list_rebuilds;
             } else if (from_t) {
+#ifdef GICP_TAIL
+                if (A.tail && l == 0) atomicAdd(&s_walk[8], 1u);
+#endif
                 // the seed's list becomes this tile's: every target tile within rt - ex of the wave box (at this
                 // pass's pose) lies within rt of S's box, so it is in the list
                 if (l < nl) A.list[(int64_t)T * kListMax + l] = ent;
@@ -2397,7 +2411,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     GICP_TAIL_MARK(1);
 #ifdef GICP_TAIL
-    if (A.tail && threadIdx.x < 7 && s_walk[threadIdx.x]) atomicAdd(A.tail + 9 + threadIdx.x, (unsigned long long)s_walk[threadIdx.x]);
+    if (A.tail && threadIdx.x < 9 && s_walk[threadIdx.x]) atomicAdd(A.tail + 9 + threadIdx.x, (unsigned long long)s_walk[threadIdx.x]);
 #endif
     __syncthreads();
     // one level when a few round trips of the final workgroup's loads cover every unit (kFlatUnits), else
