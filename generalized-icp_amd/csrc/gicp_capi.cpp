@@ -38,7 +38,6 @@ hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t, double*);
 hipError_t launch_peer_probe(const PeerArgs&, double*, hipStream_t);
 hipError_t launch_graph_pack(const GraphArgs&, hipStream_t);
-hipError_t launch_tgt_lists(const DevCloud&, float, int32_t*, int32_t*, float*, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
                               int64_t*, hipStream_t);
@@ -184,16 +183,11 @@ struct Cloud {
     uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows
     int32_t* nbi = nullptr;           // ... and their sorted indices
     bool graph_ready = false;
-    int32_t* tl_list = nullptr;       // target-side tile lists (targets only)
-    int32_t* tl_len = nullptr;
-    float* tl_r = nullptr;
-    bool tl_ready = false;
     bool cov_ready = false;
     int cov_shard = 0, cov_nshards = 1;  // whose tiles' covariances were computed (build_cloud)
 
     size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
     size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0, cap_boxes = 0, cap_seed = 0;
-    size_t cap_tll = 0, cap_tln = 0, cap_tlr = 0;
     void reserve_points(int64_t np) {
         dreserve(xyz64, cap_xyz, (size_t)np * 4);
         dreserve(rel32, cap_rel, (size_t)np);
@@ -222,11 +216,6 @@ struct Cloud {
         dfree(seed_tab);
         dfree(nbq);
         dfree(nbi);
-        dfree(tl_list);
-        dfree(tl_len);
-        dfree(tl_r);
-        cap_tll = cap_tln = cap_tlr = 0;
-        tl_ready = false;
         cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
         cap_nbq = cap_nbi = cap_boxes = cap_seed = 0;
         n = 0;
@@ -247,9 +236,6 @@ struct Cloud {
         v.seed_shift = seed_shift;
         v.nbq = graph_ready ? nbq : nullptr;
         v.nbi = graph_ready ? nbi : nullptr;
-        v.tl_list = tl_ready ? tl_list : nullptr;
-        v.tl_len = tl_ready ? tl_len : nullptr;
-        v.tl_r = tl_ready ? tl_r : nullptr;
         v.n = n;
         v.ntiles = ntiles;
         v.nblocks = nblocks;
@@ -349,7 +335,6 @@ struct gicp_ctx {
     int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
-    double kappa_far_frac = 0.04;     // ... for lanes the graph could not prove (GICP_CERT_KAPPA_FAR)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
     BuildScratch bs;
@@ -372,7 +357,6 @@ struct gicp_ctx {
         int64_t M = 0;
         int dim = 0;
         bool graph = false;
-        double tlists = 0.0;
         int device = 0;
         gicp_params p{};
         int rc = GICP_OK;
@@ -396,9 +380,6 @@ struct gicp_ctx {
     size_t cap_hint = 0, cap_list = 0, cap_llen = 0, cap_lpass = 0, cap_lrc = 0;
     int pass = 0;
     bool use_lists = true;
-    bool use_tlists = true;           // GICP_NO_TLISTS=1: no target-side tile lists (first passes walk the hierarchy)
-    double tlist_frac = 2.0;          // their radius, a multiple of d_c (GICP_TLIST_R)
-    double tlists() const { return use_lists && use_tlists ? tlist_frac : 0.0; }
     double skin_frac = 0.2;           // candidate-list skin as a fraction of d_c (GICP_SKIN)
     double skin_gain = 1.0;           // adaptive skin: multiple of the tile's last displacement (GICP_SKIN_GAIN)
     double last_rebuilds = 0.0;
@@ -619,8 +600,7 @@ int shard_tile_count(int ntiles, int shard, int nshards) {
 // rank needs the whole cloud's index for the neighbourhoods, but only its own tiles' covariances); the other
 // rows read NaN.
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
-                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1,
-                 double tlists = 0.0 /* target-side lists of radius tlists x d_c (0: none) */) {
+                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -638,7 +618,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
     cl.n = 0;   // buffers are kept (grow-only) and reused
     cl.cov_ready = false;
     cl.graph_ready = false;
-    cl.tl_ready = false;
     cl.dim = dim;
     cl.bits = dim == 3 ? 10 : 16;
     // one fused, branch-free pass: bounds and the finiteness test (v - v is NaN for NaN and +-inf)
@@ -740,15 +719,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         }
         HIPCHK(launch_build_tiles(d_in, dim, cl.perm, cl.tiles, cl.boxes, cl.ntiles, cl.xyz64, cl.rel32, cl.inv, d_rho, st));
         HIPCHK(launch_build_blocks(cl.tiles, cl.ntiles, cl.blocks, cl.nblocks, dim, st));
-        if (tlists > 0.0) {   // target-side tile lists: every target tile near each tile, nearest first (§3f)
-            const double tl_frac = tlists;   // radius as a multiple of d_c
-            dreserve(cl.tl_list, cl.cap_tll, (size_t)cl.ntiles * kListMax);
-            dreserve(cl.tl_len, cl.cap_tln, (size_t)cl.ntiles);
-            dreserve(cl.tl_r, cl.cap_tlr, (size_t)cl.ntiles);
-            const double dc = p.max_distance_correspondence;
-            const float R = (float)std::min(tl_frac * dc, 1e30);
-            HIPCHK(launch_tgt_lists(cl.view(), R, cl.tl_list, cl.tl_len, cl.tl_r, st));
-        }
         unsigned rho_bits = 0;
         HIPCHK(hipMemcpyAsync(&rho_bits, d_rho, sizeof(unsigned), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -812,7 +782,6 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         cl.cov_shard = cov_shard;
         cl.cov_nshards = cov_nshards;
         cl.graph_ready = graph;
-        cl.tl_ready = tlists > 0.0;
         tick(graph ? "covariances+graph" : "covariances");
         if (verbose)
             std::fprintf(stderr, "[gicp] cloud n=%lld tiles=%d (%.2fx min) extent cap=%d cells rho=%.4f | ms:%s\n",
@@ -907,7 +876,6 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.mg = make_margin(d, c->src.rho, c->tgt.rho, dc + kappa);
     a.search2 = screen_bound(a.mg, dc + kappa);
     a.kappa = (float)kappa;
-    a.kappa_far = (float)std::min(std::max(kappa, c->use_certs ? c->kappa_far_frac * dc : 0.0), dc);
     a.empty_r = (float)dc * (1.0f + 1e-6f);
     if (c->use_certs) {
         a.cert_j = c->d_cert_j;
@@ -1182,8 +1150,6 @@ int gicp_create(gicp_ctx** out, int device) {
     if (!c) return GICP_E_NOMEM;
     c->device = device;
     if (const char* e = std::getenv("GICP_NO_LISTS")) c->use_lists = !(e[0] == '1');
-    if (const char* e = std::getenv("GICP_NO_TLISTS")) c->use_tlists = !(e[0] == '1');
-    if (const char* e = std::getenv("GICP_TLIST_R")) c->tlist_frac = std::atof(e) > 0.0 ? std::atof(e) : 2.0;
     if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
@@ -1193,7 +1159,6 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
-    if (const char* e = std::getenv("GICP_CERT_KAPPA_FAR")) c->kappa_far_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;
@@ -1329,8 +1294,7 @@ int gicp_set_target(gicp_ctx* c, const double* xyz, int64_t M, int dim, const gi
     return guard_impl(c, "gicp_set_target", [&] {
         c->ptgt = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs, c->bs, c->stream, false, 0, 1,
-                    c->tlists());
+        build_cloud(c->tgt, xyz, M, dim, c->ptgt, c->use_graph && c->use_certs, c->bs, c->stream);
         if (c->src.n) reset_tile_state(c);
     });
 }
@@ -1705,7 +1669,7 @@ void staged_worker(gicp_ctx::Staged* gp) {
         std::string err;
         try {
             HIPCHK(hipSetDevice(gp->device));
-            build_cloud(gp->cl, gp->xyz, gp->M, gp->dim, gp->p, gp->graph, gp->bs, gp->stream, true, 0, 1, gp->tlists);
+            build_cloud(gp->cl, gp->xyz, gp->M, gp->dim, gp->p, gp->graph, gp->bs, gp->stream, true);
         } catch (const Fail& f) {
             rc = f.code;
             err = f.msg;
@@ -1773,7 +1737,6 @@ int gicp_stage_target_ex(gicp_ctx* c, const double* xyz, int64_t M, int dim, con
             g.M = M;
             g.dim = dim;
             g.graph = c->use_graph && c->use_certs;
-            g.tlists = c->tlists();
             g.device = c->device;
             g.p = prm;
             g.rc = GICP_OK;

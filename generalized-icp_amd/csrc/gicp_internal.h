@@ -94,11 +94,6 @@ struct DevCloud {
     // entry k (-1 unused).
     const uint4* nbq;         // [n][8]
     const int32_t* nbi;       // [n][kGraphK]
-    // target-side tile lists (target only; null when not built), DESIGN.md §3f: tl_list[S][kListMax] the target
-    // tiles near tile S nearest first, tl_len[S] how many, tl_r[S] the box gap below which every tile is listed
-    const int32_t* tl_list;
-    const int32_t* tl_len;
-    const float* tl_r;
     int64_t n;
     int32_t ntiles;
     int32_t nblocks;
@@ -264,7 +259,6 @@ struct CorrArgs {
     float* cert_gap;          // [src.n] runner-up gap (found) or empty radius R (none), relative to cert_pass
     int32_t* cert_pass;       // [src.ntiles] pass the tile's certificates refer to (-1: none)
     float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
-    float kappa_far;          // ... for lanes the graph descent left at an unproved local minimum (<= kappa: off)
     float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected
     unsigned long long* stamps;  // [waves][16] phase cycles + counters (STAMPS diagnostic build only; else null)
     // 1: the final workgroup also runs the inner solve + pose update (what k_solve does), when no exchange
@@ -279,9 +273,8 @@ struct CorrArgs {
 // then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
 // sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] why lanes walked
 // (counts, k_corr: no last match / descent local minimum without proof / uncovered near tie / hops exhausted /
-// walking lanes / walking waves / waves with one walking lane); [16] waves that scanned a target-side list,
-// [17] of which it certified (the tile adopted it)
-constexpr int kTailWords = 20;
+// walking lanes / walking waves / waves with one walking lane)
+constexpr int kTailWords = 16;
 
 constexpr int nstat(int D) {
     return (D * (D + 1) / 2) * (D * (D + 1) / 2) + (D * (D + 1) / 2) * D + (D * (D + 1) / 2) + D * D + D + 2;

@@ -73,13 +73,6 @@ __device__ __forceinline__ double wave_maxd(double v) {
     return v;
 }
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
-// the wave's LDS writes before its later LDS reads by other lanes: the compiler must not move LDS accesses
-// across (memory clobbers; the wave barrier alone is not a memory operation to it)
-__device__ __forceinline__ void lds_sync() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
 // ascending bitonic sort of one (key, val) pair per lane across the wave; ties by val (deterministic)
 __device__ __forceinline__ void wave_sort64(float& key, int& val) {
     const int l = __lane_id();
@@ -1188,112 +1181,6 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
 }
 
 // ---------------------------------------------------------------------------
-// target-side tile lists: for every target tile S, the target tiles whose boxes lie within a
-// radius of S's box, nearest first, and the radius r(S) they certify: every target tile whose box gap to S's
-// box is below r(S) is in the list.  k_corr's first pass (no last matches, no source-side list yet) scans the
-// list of its Morton seed tile instead of walking the box hierarchy, whenever the wave's box lies within
-// r(S) - (its final search radius) of S's box.  Built once per target cloud, one wave per tile.
-// ---------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ float box_gap(const double* ca, const float* ha, const double* cb, const float* hb) {
-    float g2 = 0.f;
-#pragma unroll
-    for (int a = 0; a < D; ++a) {
-        const float e = fmaxf((float)fabs(ca[a] - cb[a]) - ha[a] - hb[a], 0.f);
-        g2 = fmaf(e, e, g2);
-    }
-    return __builtin_amdgcn_sqrtf(g2);
-}
-
-constexpr int kTlistCand = 256;   // candidates a wave collects before it shrinks the radius
-
-template <int D>
-__global__ void __launch_bounds__(256) k_tgt_lists(DevCloud cl, float R, int32_t* __restrict__ out_list,
-                                                   int32_t* __restrict__ out_len, float* __restrict__ out_r) {
-    __shared__ float s_key[kWavesPerWG][kTlistCand];
-    __shared__ int s_idx[kWavesPerWG][kTlistCand];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int S = blockIdx.x * kWavesPerWG + w;
-    if (S >= cl.ntiles) return;   // (wave-uniform)
-    const TileBox me = cl.boxes[S];
-    const uint64_t lt = (1ull << l) - 1ull;
-    float Rc = R;
-    int ncand = 0;
-    for (;;) {   // collect the tiles within Rc (a wave-uniform loop: shrinks Rc when more than kTlistCand)
-        ncand = 0;
-        for (int b0 = 0; b0 < cl.nblocks; b0 += 64) {
-            const int b = b0 + l;
-            bool hit = false;
-            if (b < cl.nblocks) {
-                const BlockInfo bi = cl.blocks[b];
-                hit = box_gap<D>(me.c, me.h, bi.c, bi.h) <= Rc;
-            }
-            uint64_t m = __ballot(hit);
-            while (m) {
-                const int bb = b0 + __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                const int t = bb * kBlockTiles + l;
-                float g = 3e38f;
-                if (t < cl.ntiles) g = box_gap<D>(me.c, me.h, cl.boxes[t].c, cl.boxes[t].h);
-                const bool in = g <= Rc;
-                const uint64_t mi = __ballot(in);
-                const int pos = ncand + __popcll(mi & lt);
-                if (in && pos < kTlistCand) {
-                    s_key[w][pos] = g;
-                    s_idx[w][pos] = t;
-                }
-                ncand += __popcll(mi);
-            }
-        }
-        if (ncand <= kTlistCand) break;
-        Rc *= 0.75f;
-    }
-    lds_sync();
-    // more than kListMax candidates: the radius shrinks to the (kListMax + 1)-th smallest gap (a radix select on
-    // the float bits over the <= kTlistCand collected), and only the gaps below it are kept
-    float rcert = Rc;
-    if (ncand > kListMax) {
-        unsigned lo = 0u, hi = __float_as_uint(Rc) + 1u;   // count(key < hi) > kListMax >= count(key < lo)
-        while (hi - lo > 1u) {
-            const unsigned mid = lo + ((hi - lo) >> 1);
-            int c = 0;
-            for (int k = l; k < ncand; k += 64) c += __float_as_uint(s_key[w][k]) < mid;
-            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-            if (c <= kListMax) lo = mid;
-            else hi = mid;
-        }
-        rcert = __uint_as_float(lo);   // count(key < rcert) <= kListMax: every tile with a smaller gap is kept
-    }
-    // compact the kept candidates (key < rcert, or all when they fit) in place (a kept entry moves to a
-    // position no later than its own, and each round reads before it writes), then sort them nearest first
-    int n = 0;
-    for (int k0 = 0; k0 < ncand; k0 += 64) {
-        const int k = k0 + l;
-        const bool keep = k < ncand && (ncand <= kListMax || __float_as_uint(s_key[w][k]) < __float_as_uint(rcert));
-        const uint64_t mk = __ballot(keep);
-        const int pos = n + __popcll(mk & lt);
-        const float kk = keep ? s_key[w][k] : 0.f;
-        const int kv = keep ? s_idx[w][k] : 0;
-        lds_sync();
-        if (keep) {
-            s_key[w][pos] = kk;
-            s_idx[w][pos] = kv;
-        }
-        lds_sync();
-        n += __popcll(mk);
-    }
-    float key = l < n ? s_key[w][l] : 3e38f;
-    int val = l < n ? s_idx[w][l] : 0x7fffffff;
-    wave_sort64(key, val);
-    if (l < n) out_list[(int64_t)S * kListMax + l] = val;
-    if (l == 0) {
-        out_len[S] = n;
-        // rounding slack of the fp32 gaps (coordinates of tens of metres: a few 1e-6 m)
-        out_r[S] = fmaxf(rcert * 0.9999f - 1e-5f, 0.f);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // per-iteration correspondences + weights + statistics
 // ---------------------------------------------------------------------------
 // Register budget of k_corr: on gfx950 a wave with next_free_sgpr >= 94 leaves 6 waves per SIMD,
@@ -1487,8 +1374,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
 #ifdef GICP_TAIL
     unsigned long long tl[kTailWords] = {};
-    __shared__ unsigned s_walk[9];
-    if (threadIdx.x < 9) s_walk[threadIdx.x] = 0;
+    __shared__ unsigned s_walk[8];
+    if (threadIdx.x < 8) s_walk[threadIdx.x] = 0;
     __syncthreads();
     if (A.tail && blockIdx.x == 0 && threadIdx.x == 0) A.tail[0] = __builtin_amdgcn_s_memrealtime();   // (first dispatched)
 #define GICP_TAIL_MARK(k) do { if (A.tail) tl[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -1619,7 +1506,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // certificate: every other target is >= min(runner-up, r(j) - d(p', j)) - e away.
         bool gcert = false;
         float ggap = 0.f;
-        bool lmin = false;   // the descent ended at a local minimum it could not prove (a point far from the surface)
 #ifdef GICP_TAIL
         int gwhy = 0;   // diagnostic: how the descent ended for a lane it did not prove
 #define GICP_WHY(k) (gwhy = (k))
@@ -1739,7 +1625,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         act = false;
                     } else if (bk < 0) {
                         act = false;                              // local minimum without proof
-                        lmin = true;
                         GICP_WHY(1);
                     } else {                                      // hop: p' relative to the nearer candidate
                         qr[0] = bx;
@@ -1826,12 +1711,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         nwalked = skip_walk ? 0 : 1;
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
         // farther than kappa since its last pass (the pose is still converging) walks without it
-        // A lane the descent could not prove at a local minimum (its nearest target is too far for the
-        // graph row's radius) walks, and its runner-up gap is resolved only up to the widening: with kappa
-        // its certificate would break again after a displacement of kappa / 2, and the lane would walk in
-        // pass after pass.  Such lanes widen by kappa_far instead, so their certificate outlasts the settling.
-        const float kw = lmin ? A.kappa_far : A.kappa;
-        const float kap = cdelta > kw ? 0.f : kw;
+        const float kap = cdelta > A.kappa ? 0.f : A.kappa;
 
         // ---- fp32 screen: best and runner-up keys -------------------------
         const unsigned init = __float_as_uint(A.search2) | 63u;
@@ -1906,37 +1786,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         bool use = false;
         float delta = 0.f, rc = 0.f;
         int nl = 0;
-        const int32_t* lbase = A.list + (int64_t)T * kListMax;
         if (lists && !skip_walk) {
             nl = A.list_len[T];
             rc = A.list_rcert[T];
             if (nl > 0 && rc > 0.f) {
                 delta = disp_since(A.list_pass[T]);
                 use = delta >= 0.f && delta < rc;
-            }
-        }
-        // no usable list of this source tile (its first pass, or it moved out of its list): the target-side
-        // list of the seed tile S certifies every target tile within rt of S's box, and every
-        // point of the wave box lies within `ex` of S's box, so it serves whenever ex + the final search radius
-        // stays below rt (checked after the scan, exactly like the tile's own list with delta = ex)
-        bool from_t = false;
-        if (lists && !use && !skip_walk && tg.tl_len) {
-            const int S = __builtin_amdgcn_readfirstlane(seed);
-            const int ntl = tg.tl_len[S];
-            const float rt = tg.tl_r[S];
-            float ex2 = 0.f;
-#pragma unroll
-            for (int a = 0; a < D; ++a) {
-                const float e = fmaxf((float)fabs(q.ow[a] - tg.boxes[S].c[a]) + q.ew[a] - tg.boxes[S].h[a], 0.f);
-                ex2 = fmaf(e, e, ex2);
-            }
-            const float ex = __builtin_amdgcn_sqrtf(ex2) * 1.0001f + 1e-6f;
-            if (ntl > 0 && ex < rt) {
-                use = from_t = true;
-                nl = ntl;
-                rc = rt;
-                delta = ex;
-                lbase = tg.tl_list + (int64_t)S * kListMax;
             }
         }
         int ent = 0;   // lane k: list entry k (when the list is used)
@@ -1948,21 +1803,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             float eg2 = 3e38f;
             const Query<D> qa = active_box<D>(q, lb >= 0.f);   // the searching lanes' box
             if (l < nl) {
-                ent = lbase[l];
+                ent = A.list[(int64_t)T * kListMax + l];
                 eg2 = gap2_box<D>(qa, tg.tiles[ent].c, tg.tiles[ent].h);
                 est = tg.tiles[ent].start;
                 ecnt = tg.tiles[ent].count;
-            }
-#ifdef GICP_TAIL
-            if (from_t && A.tail && l == 0) atomicAdd(&s_walk[7], 1u);
-#endif
-            if (from_t) {   // the seed's list is ordered from S's box: reorder it nearest-first to this wave's box,
-                            // so the scan's bound falls fast (and the list this tile adopts is ordered for it)
-                int src = l;
-                wave_sort64(eg2, src);
-                ent = __shfl(ent, src);
-                est = __shfl(est, src);
-                ecnt = __shfl(ecnt, src);
             }
             float wb = wave_maxf(lb);
             uint64_t rem = __ballot(l < nl && eg2 <= wb);
@@ -1998,18 +1842,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 lb = lane_bound();
                 lbx = inflate(lb);
                 ++list_rebuilds;
-            } else if (from_t) {
-#ifdef GICP_TAIL
-                if (A.tail && l == 0) atomicAdd(&s_walk[8], 1u);
-#endif
-                // the seed's list becomes this tile's: every target tile within rt - ex of the wave box (at this
-                // pass's pose) lies within rt of S's box, so it is in the list
-                if (l < nl) A.list[(int64_t)T * kListMax + l] = ent;
-                if (l == 0) {
-                    A.list_len[T] = nl;
-                    A.list_rcert[T] = fmaxf((rc - delta) * 0.9999f, 0.f);
-                    A.list_pass[T] = A.pass;
-                }
             }
         }
         if (!use && !skip_walk) {
@@ -2411,7 +2243,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     GICP_TAIL_MARK(1);
 #ifdef GICP_TAIL
-    if (A.tail && threadIdx.x < 9 && s_walk[threadIdx.x]) atomicAdd(A.tail + 9 + threadIdx.x, (unsigned long long)s_walk[threadIdx.x]);
+    if (A.tail && threadIdx.x < 7 && s_walk[threadIdx.x]) atomicAdd(A.tail + 9 + threadIdx.x, (unsigned long long)s_walk[threadIdx.x]);
 #endif
     __syncthreads();
     // one level when a few round trips of the final workgroup's loads cover every unit (kFlatUnits), else
@@ -2781,14 +2613,6 @@ hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blo
     const unsigned g2 = (unsigned)((nsuper + kWavesPerWG - 1) / kWavesPerWG);
     hipLaunchKernelGGL(k_build_blocks<BlockInfo>, dim3(g2), dim3(256), 0, st, (const BlockInfo*)blocks, nblocks,
                        blocks + nblocks, nsuper, dim);
-    return hipGetLastError();
-}
-
-hipError_t launch_tgt_lists(const DevCloud& cl, float R, int32_t* list, int32_t* len, float* r, hipStream_t st) {
-    if (cl.ntiles <= 0) return hipSuccess;
-    const unsigned g = (unsigned)((cl.ntiles + kWavesPerWG - 1) / kWavesPerWG);
-    if (cl.dim == 2) hipLaunchKernelGGL(k_tgt_lists<2>, dim3(g), dim3(256), 0, st, cl, R, list, len, r);
-    else hipLaunchKernelGGL(k_tgt_lists<3>, dim3(g), dim3(256), 0, st, cl, R, list, len, r);
     return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ def main():
         evs.append(np.array(e.iteration_times()) * 1e3)
     del os.environ["GICP_TAIL_DUMP"]
     for r in range(a.reps):
-        recs.append(np.fromfile(os.path.join(d, f"tail.{r}"), dtype=np.uint64).reshape(-1, 20).astype(np.int64))
+        recs.append(np.fromfile(os.path.join(d, f"tail.{r}"), dtype=np.uint64).reshape(-1, 16).astype(np.int64))
     e.close()
     R = np.stack(recs)            # [rep][iter][16]
     ev = np.stack(evs)            # [rep][iter] us
@@ -68,11 +68,10 @@ def main():
         ev[:, conv].mean(), span[:, conv].mean(), waves[:, conv].mean(), us(R[:, conv, 8] - R[:, conv, 1]).mean()) +
         " ".join(f"{n} {s[:, conv].mean():.2f}" for n, s in zip(names, steps)))
     print("launch overhead (event - span), converged mean: %.1f us" % (ev[:, conv] - span[:, conv]).mean())
-    print("why lanes walked (rep 0): iter | no-last-match  local-min  uncovered-tie  hops | lanes  waves  1-lane-waves"
-          " | target-list waves  certified")
+    print("why lanes walked (rep 0): iter | no-last-match  local-min  uncovered-tie  hops | lanes  waves  1-lane-waves")
     for i in range(R.shape[1]):
-        w = R[0, i, 9:18]
-        print(f"{i:4d} | {w[0]:8d} {w[1]:8d} {w[2]:8d} {w[3]:8d} | {w[4]:8d} {w[5]:7d} {w[6]:7d} | {w[7]:7d} {w[8]:7d}")
+        w = R[0, i, 9:16]
+        print(f"{i:4d} | {w[0]:8d} {w[1]:8d} {w[2]:8d} {w[3]:8d} | {w[4]:8d} {w[5]:7d} {w[6]:7d}")
 
 
 if __name__ == "__main__":

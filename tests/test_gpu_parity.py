@@ -308,15 +308,12 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
     A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
     default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
-    certificates or lists (plain full walks), one without the target graph's descent, and ones without
-    target-side tile lists or with lists so short that most first-pass scans fall back, while the
+    certificates or lists (plain full walks), and one without the target graph's descent, while the
     certified passes evaluate far fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1", "plain", "nograph", "notlists", "tlists_small"):
-        monkeypatch.setenv("GICP_NO_TLISTS", "1" if flag == "notlists" else "0")
-        monkeypatch.setenv("GICP_TLIST_R", "0.25" if flag == "tlists_small" else "2.0")   # small: most fall back
+    for flag in ("0", "1", "plain", "nograph"):
         monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "nograph" else "0")
         monkeypatch.setenv("GICP_NO_CERTS", "1" if flag in ("1", "plain") else "0")
         monkeypatch.setenv("GICP_NO_LISTS", "1" if flag == "plain" else "0")
@@ -335,7 +332,7 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    for other in ("1", "plain", "nograph", "notlists", "tlists_small"):
+    for other in ("1", "plain", "nograph"):
         assert np.array_equal(out["0"][0], out[other][0])
         for a, b in zip(out["0"][1], out[other][1]):
             assert np.array_equal(a, b)
