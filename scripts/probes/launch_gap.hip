@@ -11,6 +11,15 @@ struct Big {
     double v[87];   // ~700 B, like CorrArgs
     int* out;
 };
+template <int N>
+struct Arg {
+    double v[N];
+    int* out;
+};
+template <int N>
+__global__ void k_arg(Arg<N> b) {
+    if (b.out && threadIdx.x == 1000000) b.out[0] = (int)b.v[N - 1];
+}
 
 __global__ void k_empty(int* out) {
     if (out && threadIdx.x == 1000000) out[0] = 1;
@@ -83,6 +92,18 @@ int main() {
     for (int g : {79, 527, 625, 1536, 5000})
         printf("empty %4d WG x 256     : %.2f us\n", g, period([&] { hipLaunchKernelGGL(k_empty, dim3(g), dim3(256), 0, 0, d_out); }, n));
     printf("700-B arg, 79 WG x 256 : %.2f us\n", period([&] { hipLaunchKernelGGL(k_big, dim3(79), dim3(256), 0, 0, b); }, n));
+    {
+        Arg<7> a8{};   a8.out = d_out;
+        Arg<15> a16{}; a16.out = d_out;
+        Arg<31> a32{}; a32.out = d_out;
+        Arg<47> a48{}; a48.out = d_out;
+        Arg<63> a64{}; a64.out = d_out;
+        printf("64-B arg, 79 WG        : %.2f us\n", period([&] { hipLaunchKernelGGL(k_arg<7>, dim3(79), dim3(256), 0, 0, a8); }, n));
+        printf("128-B arg, 79 WG       : %.2f us\n", period([&] { hipLaunchKernelGGL(k_arg<15>, dim3(79), dim3(256), 0, 0, a16); }, n));
+        printf("256-B arg, 79 WG       : %.2f us\n", period([&] { hipLaunchKernelGGL(k_arg<31>, dim3(79), dim3(256), 0, 0, a32); }, n));
+        printf("384-B arg, 79 WG       : %.2f us\n", period([&] { hipLaunchKernelGGL(k_arg<47>, dim3(79), dim3(256), 0, 0, a48); }, n));
+        printf("512-B arg, 79 WG       : %.2f us\n", period([&] { hipLaunchKernelGGL(k_arg<63>, dim3(79), dim3(256), 0, 0, a64); }, n));
+    }
     printf("1 KB write, 79 WG      : %.2f us\n", period([&] { hipLaunchKernelGGL(k_write, dim3(79), dim3(256), 0, 0, d_buf); }, n));
     printf("1 KB write, 1536 WG    : %.2f us\n", period([&] { hipLaunchKernelGGL(k_write, dim3(1536), dim3(256), 0, 0, d_buf); }, n));
     printf("ticket, 79 WG          : %.2f us\n", period([&] { hipLaunchKernelGGL(k_ticket, dim3(79), dim3(256), 0, 0, d_t, (double*)d_buf); }, n));
