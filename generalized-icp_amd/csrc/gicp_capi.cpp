@@ -1898,15 +1898,18 @@ int gicp_peer_init(gicp_ctx* c, int nranks, int rank, const char* handles, doubl
             int khz = 0;
             HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
             p.timeout = (uint64_t)(timeout_s * (khz > 0 ? khz : 100000) * 1e3);
-            // the probe: one exchange of (rank + 1, 1), which every rank runs now
+            // the probe: kPeerProbeRounds full-slot exchanges checked bit for bit, which every rank runs now
             if (!c->d_probe) dalloc(c->d_probe, 2);
             HIPCHK(launch_peer_probe(p, c->d_probe, c->stream));
             double got[2] = {0, 0};
             HIPCHK(hipMemcpyAsync(got, c->d_probe, sizeof(got), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
-            if (got[0] != 0.5 * nranks * (nranks + 1) || got[1] != (double)nranks)
-                throw Fail{GICP_E_COMM, "peer exchange probe failed (got " + std::to_string(got[0]) + ", " +
-                                            std::to_string(got[1]) + ")"};
+            if (got[0] != (double)kPeerProbeRounds || got[1] != 0.0)
+                throw Fail{GICP_E_COMM, got[0] < 0.0 ? std::string("peer exchange probe failed (a rank did not arrive)")
+                                                     : "peer exchange probe failed (" + std::to_string((int)got[1]) +
+                                                           " of " + std::to_string(kPeerSlot * kPeerProbeRounds) +
+                                                           " summed values wrong after " +
+                                                           std::to_string((int)got[0]) + " rounds)"};
         } catch (...) {
             close_peers(c);
             throw;

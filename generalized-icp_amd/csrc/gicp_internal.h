@@ -201,6 +201,7 @@ constexpr int kTicketStride = 32;
 constexpr int kMaxPeers = GICP_MAX_PEERS;
 constexpr int kPeerSlot = 80;
 constexpr int kPeerFlagWords = 2 * kMaxPeers;   // doubles before the slots
+constexpr int kPeerProbeRounds = 8;             // full-slot exchanges gicp_peer_init's probe runs (both parities)
 constexpr size_t kPeerAreaDoubles = kPeerFlagWords + (size_t)2 * kMaxPeers * kPeerSlot;
 struct PeerArgs {
     double* const* area;       // device array [n]: rank p's area as mapped here (area[rank] = this rank's own)

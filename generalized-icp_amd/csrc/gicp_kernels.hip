@@ -1286,20 +1286,45 @@ __device__ bool peer_exchange(const PeerArgs P, uint64_t seq, double* vals) {   
     return true;
 }
 
-// gicp_peer_init's probe: one exchange of (rank + 1, 1) -> out = (sum, ranks), or (-1, -1) on a timeout
-__global__ void __launch_bounds__(64) k_peer_probe(PeerArgs P, double* out) {
-    __shared__ double v[2];
+// gicp_peer_init's probe: `rounds` back-to-back exchanges of a full slot (kPeerSlot values, both parities), each
+// value a pattern of (rank, value index, round) whose sum over the ranks is exact in fp64, so every summed
+// value must come back bit-exact: a mapping, store ordering or flag protocol that misbehaves across the
+// devices shows up here before the first registration.  out = (rounds completed, or -1 on a timeout; values
+// that came back wrong).
+__device__ __forceinline__ double probe_value(int rank, int k, int r) {
+    return ldexp((double)((rank + 1) * 1000003 + k * 97 + r * 7919), -7);
+}
+__global__ void __launch_bounds__(64) k_peer_probe(PeerArgs P, int rounds, double* out) {
+    __shared__ double v[kPeerSlot];
     __shared__ uint64_t s_seq;
+    __shared__ int s_bad;
     if (threadIdx.x == 0) {
-        v[0] = (double)(P.rank + 1);
-        v[1] = 1.0;
-        s_seq = *P.ctr + 1;
+        s_seq = *P.ctr;
+        s_bad = 0;
     }
-    __syncthreads();
-    const bool ok = peer_exchange<2>(P, s_seq, v);
+    int done = 0;
+    for (int r = 0; r < rounds; ++r) {
+        for (int k = threadIdx.x; k < kPeerSlot; k += blockDim.x) v[k] = probe_value(P.rank, k, r);
+        __syncthreads();
+        if (threadIdx.x == 0) ++s_seq;
+        __syncthreads();
+        if (!peer_exchange<kPeerSlot>(P, s_seq, v)) {
+            done = -1;
+            break;
+        }
+        int bad = 0;
+        for (int k = threadIdx.x; k < kPeerSlot; k += blockDim.x) {
+            double want = 0.0;
+            for (int p = 0; p < P.n; ++p) want += probe_value(p, k, r);
+            bad += v[k] != want;
+        }
+        if (bad) atomicAdd(&s_bad, bad);
+        __syncthreads();
+        done = r + 1;
+    }
     if (threadIdx.x == 0) {
-        out[0] = ok ? v[0] : -1.0;
-        out[1] = ok ? v[1] : -1.0;
+        out[0] = (double)done;
+        out[1] = (double)s_bad;
     }
 }
 
@@ -2662,7 +2687,7 @@ hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
 }
 
 hipError_t launch_peer_probe(const PeerArgs& p, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, st, p, out);
+    hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, st, p, kPeerProbeRounds, out);
     return hipGetLastError();
 }
 
