@@ -408,6 +408,7 @@ struct gicp_ctx {
     size_t cap_ttop = 0, cap_tdet = 0;
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
+    int batch_hint = 0;               // iterations the last converging align ran: its first batch next time
     // diagnostics of the last pass
     double last_amb = 0.0, last_pairs = 0.0, last_sq = 0.0, last_gproved = 0.0, last_walked = 0.0;
     float last_corr_ms = 0.f, last_reduce_ms = 0.f;
@@ -1516,11 +1517,16 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
         // from the device state, statistics reduced in-launch) [+ RCCL all-reduce] + k_solve.
         // After convergence the remaining launches of a batch exit at once.
+        // A host exchange synchronises every iteration anyway: batches of one, so the loop stops at the
+        // converged iteration without launching more.  Otherwise the first batch is as long as the last
+        // converging align on this context ran (a sequence of similar registrations -- odometry frames --
+        // then pays one host sync per call instead of two or three; a shorter registration pays a few
+        // launches that exit at once), later batches 8.
+        const int first_batch = std::max(8, std::min((int)gicp_ctx::kMaxBatch, c->batch_hint));
         while (enq < prm.max_iterations) {
-            // a host exchange synchronises every iteration anyway: batches of one, so the loop stops
-            // at the converged iteration without launching more
             const int B = std::min(prm.max_iterations - enq,
-                                   c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch : 8);
+                                   c->hook ? 1 : prm.fixed_iterations ? (int)gicp_ctx::kMaxBatch
+                                                                      : enq == 0 ? first_batch : 8);
             for (int b = 0; b < B; ++b) {
                 const int it = enq + b;
                 CorrArgs a = corr_args(c, 0);
@@ -1580,6 +1586,7 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
             if (hs.converged) break;
         }
         const auto t1 = std::chrono::steady_clock::now();
+        if (!prm.fixed_iterations && hs.converged) c->batch_hint = hs.iter;
         c->iter_ms.resize((size_t)std::max(0, std::min(hs.iter, prm.max_iterations)));
 #ifdef GICP_TAIL
         if (tail_path) {
