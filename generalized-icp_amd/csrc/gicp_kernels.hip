@@ -1511,8 +1511,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // search cap below and the graph descent start from it
         bool have_jp = false;
         float qr[3] = {0.f, 0.f, 0.f}, d2jp = 0.f;
+        uint32_t w0[16];   // the first half of jp's graph row (the descent's first step), requested with jp
         if (A.cert_j && q.valid && !cert && jp >= 0 && jp < tg.n) {
             const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[jp];
+            if (tg.nbq) {
+                const uint4* row = tg.nbq + (int64_t)jp * 8;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint4 v = row[c];
+                    w0[4 * c] = v.x;
+                    w0[4 * c + 1] = v.y;
+                    w0[4 * c + 2] = v.z;
+                    w0[4 * c + 3] = v.w;
+                }
+            }
             const double tv[3] = {t4.x, t4.y, t4.z};
 #pragma unroll
             for (int a = 0; a < D; ++a) {
@@ -1561,7 +1573,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                             w[4 * c + 3] = v.w;
                         }
                     };
-                    load_half(0);
+                    if (h == 0) {
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) w[k] = w0[k];
+                    } else {
+                        load_half(0);
+                    }
                     const float r = __uint_as_float(w[0]), sc = __uint_as_float(w[1]);
                     const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
                     float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f, rho = 0.f;
