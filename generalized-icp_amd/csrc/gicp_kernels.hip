@@ -1545,9 +1545,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         float ggap = 0.f;
 #ifdef GICP_TAIL
         int gwhy = 0;   // diagnostic: how the descent ended for a lane it did not prove
+        int gout = 0;   // ... and for one it proved: 1 at the start node's local minimum, 2 at a row entry of
+                        // the start node, 3 after a hop, 4 a near tie resolved exactly
 #define GICP_WHY(k) (gwhy = (k))
+#define GICP_OUT(k) (gout = (k))
 #else
 #define GICP_WHY(k) ((void)0)
+#define GICP_OUT(k) ((void)0)
 #endif
         if (tg.nbq && wave_any(have_jp)) {
             bool act = have_jp;
@@ -1662,6 +1666,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         if (!tie) GICP_WHY(2);
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
+                        GICP_OUT(h > 0 ? 3 : bk < 0 ? 1 : 2);
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
                         ggap = fminf(e2, r - d0) - e1 - 2.f * e;
                         act = false;
@@ -1718,6 +1723,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         if (t >= 0) consider(t);
                     }
                     gcert = bj >= 0;
+                    if (gcert) GICP_OUT(4);
                     cj = bj;
                     const double g = (fmin(sqrt(sd2), (double)tfar) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
                     ggap = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
@@ -1735,18 +1741,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         // [11] a near tie the row does not cover, [12] hops exhausted, [13] walking lanes,
                         // [14] walking waves, [15] walking waves with one walking lane (per-wave counts into the
                         // workgroup's LDS, one global add per workgroup at its end)
+            // [9] lanes that descended, [10..13] proved by gout 1..4, [14] walking lanes, [15] walking waves
             const bool wl = q.valid && !cert;
-            const int why = !wl ? -1 : (jp < 0 ? 0 : (gwhy ? gwhy : -1));
             const uint64_t wm = __ballot(wl);
-            for (int k = 0; k < 4; ++k) {
-                const int c = __popcll(__ballot(why == k));
+            const int cd = __popcll(__ballot(have_jp));
+            if (l == 0 && cd) atomicAdd(&s_walk[0], (unsigned)cd);
+            for (int k = 1; k <= 4; ++k) {
+                const int c = __popcll(__ballot(gout == k));
                 if (l == 0 && c) atomicAdd(&s_walk[k], (unsigned)c);
             }
             if (l == 0 && wm) {
-                atomicAdd(&s_walk[4], (unsigned)__popcll(wm));
-                atomicAdd(&s_walk[5], 1u);
-                if (__popcll(wm) == 1) atomicAdd(&s_walk[6], 1u);
+                atomicAdd(&s_walk[5], (unsigned)__popcll(wm));
+                atomicAdd(&s_walk[6], 1u);
             }
+            (void)gwhy;
         }
 #endif
         ngproved = __popcll(__ballot(gcert));

@@ -68,7 +68,7 @@ def main():
         ev[:, conv].mean(), span[:, conv].mean(), waves[:, conv].mean(), us(R[:, conv, 8] - R[:, conv, 1]).mean()) +
         " ".join(f"{n} {s[:, conv].mean():.2f}" for n, s in zip(names, steps)))
     print("launch overhead (event - span), converged mean: %.1f us" % (ev[:, conv] - span[:, conv]).mean())
-    print("why lanes walked (rep 0): iter | no-last-match  local-min  uncovered-tie  hops | lanes  waves  1-lane-waves")
+    print("descent outcomes (rep 0): iter | descending | proved: start-node-min  start-row  after-hop  tie | walking lanes  waves")
     for i in range(R.shape[1]):
         w = R[0, i, 9:16]
         print(f"{i:4d} | {w[0]:8d} {w[1]:8d} {w[2]:8d} {w[3]:8d} | {w[4]:8d} {w[5]:7d} {w[6]:7d}")
