@@ -7,7 +7,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-prof}
-PD=${2:-profiles/r04}
+PD=${2:-profiles/r05}
 STEPS=${STEPS:-20}
 WARMUP=${WARMUP:-5}
 CMD="bench.py --gpus 1 --steps $STEPS --warmup $WARMUP"
