@@ -9,6 +9,7 @@ timeout -k 10 300 python bench.py --n 100000 > $OUT/bench_c2.json 2> $OUT/c2.err
 timeout -k 10 300 python bench.py --dim 2 --n 1000000 --no-cpu-baseline > $OUT/bench_2d_1m.json 2> $OUT/2d1m.err || { echo 2d 1m failed; exit 1; }
 timeout -k 10 300 python bench.py --dim 2 --n 100000 --no-cpu-baseline > $OUT/bench_2d_100k.json 2> $OUT/2d100k.err || { echo 2d 100k failed; exit 1; }
 timeout -k 10 400 python bench_odometry.py > $OUT/bench_odometry_staged.json 2> $OUT/odo.err || { echo odometry failed; exit 1; }
+timeout -k 10 400 python bench_odometry.py --copy > $OUT/bench_odometry_staged_copy.json 2> $OUT/odo_copy.err || { echo odometry copy failed; exit 1; }
 timeout -k 10 400 python bench_odometry.py --sync > $OUT/bench_odometry_sync.json 2> $OUT/odo_sync.err || { echo odometry sync failed; exit 1; }
 mkdir -p $OUT/pmc
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAVE_CYCLES -d $OUT/pmc/p1 -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/pmc/p1.log 2>&1 || { echo pmc failed; exit 1; }
