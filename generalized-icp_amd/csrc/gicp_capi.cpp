@@ -334,6 +334,7 @@ struct gicp_ctx {
     int unit_map = 0;                 // k_corr workgroup -> unit map (CorrArgs::unit_map, GICP_UNIT_MAP)
     int moving_map = 8;               // ... for the first moving_iters iterations of an align (GICP_MOVING_MAP)
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
+    int src_tile = kTile;             // source points per tile at most: 64, 32 or 16 (GICP_SRC_TILE)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
@@ -465,14 +466,14 @@ float screen_bound(const Margin& m, double d) {
 // the cap bounds the largest tile, which sets both the widest query wave and the loosest box.
 void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std::vector<int32_t>& start,
                       std::vector<int32_t>& count, std::vector<uint32_t>& first_code, int& cap_out, int k_hint,
-                      WorkerPool& pool) {
+                      WorkerPool& pool, int maxp = kTile) {
     const int64_t n = (int64_t)codes.size();
     static const double budget = [] {   // GICP_TILE_BUDGET: tile-count budget over ceil(n / 64)
         const char* e = std::getenv("GICP_TILE_BUDGET");
         const double b = e ? std::atof(e) : 1.35;
         return b >= 1.0 ? b : 1.35;
     }();
-    const int64_t target = (int64_t)(budget * std::ceil(n / 64.0)) + 2;
+    const int64_t target = (int64_t)(budget * std::ceil(n / (double)maxp)) + 2;   // (maxp <= 64 points a tile)
     // decode the grid coordinates once
     auto compact3 = [](uint32_t x) {   // inverse of the kernels' spread3
         x &= 0x09249249u;
@@ -510,7 +511,7 @@ void build_tile_table(const std::vector<uint32_t>& codes, int dim, int bits, std
                 const int n0 = std::min(lo0, v0), x0 = std::max(hi0, v0);
                 const int n1 = std::min(lo1, v1), x1 = std::max(hi1, v1);
                 const int n2 = std::min(lo2, v2), x2 = std::max(hi2, v2);
-                if (i - i0 < 64 && x0 - n0 <= E && x1 - n1 <= E && x2 - n2 <= E) {
+                if (i - i0 < maxp && x0 - n0 <= E && x1 - n1 <= E && x2 - n2 <= E) {
                     lo0 = n0, hi0 = x0, lo1 = n1, hi1 = x1, lo2 = n2, hi2 = x2;
                     continue;
                 }
@@ -600,8 +601,10 @@ int shard_tile_count(int ntiles, int shard, int nshards) {
 // cov_shard / cov_nshards: the covariances are computed for that shard's tiles only (a sharded source: every
 // rank needs the whole cloud's index for the neighbourhoods, but only its own tiles' covariances); the other
 // rows read NaN.
+// tile_points: points per tile at most (64; a source may take 32 or 16, CorrArgs / DESIGN.md §3h)
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
-                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1) {
+                 BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1,
+                 int tile_points = kTile) {
     if (!xyz || n <= 0 || (dim != 2 && dim != 3)) throw Fail{GICP_E_INVALID, "cloud must be a non-empty N x 2 or N x 3 array"};
     if (n > (int64_t)0x7FFFFFFF - 64) throw Fail{GICP_E_INVALID, "cloud too large (> 2^31 points)"};
     const bool verbose = std::getenv("GICP_VERBOSE") && std::getenv("GICP_VERBOSE")[0] == '1';
@@ -681,8 +684,10 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         tick("codes-d2h");
         std::vector<int32_t> tstart, tcount;
         std::vector<uint32_t> tcode;
-        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level, bs.cap_k_hint[dim & 3], bs.workers());
-        bs.cap_k_hint[dim & 3] = cl.level;
+        // (the extent-cap hint is kept for full-size tiles, the stream's case)
+        build_tile_table(codes, dim, cl.bits, tstart, tcount, tcode, cl.level,
+                         tile_points == kTile ? bs.cap_k_hint[dim & 3] : 0, bs.workers(), tile_points);
+        if (tile_points == kTile) bs.cap_k_hint[dim & 3] = cl.level;
         tick("tiling");
         cl.ntiles = (int)tstart.size();
         cl.nblocks = (cl.ntiles + kBlockTiles - 1) / kBlockTiles;
@@ -1159,6 +1164,10 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_UNIT_MAP")) c->unit_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_MAP")) c->moving_map = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("GICP_MOVING_ITERS")) c->moving_iters = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("GICP_SRC_TILE")) {
+        const int v = std::atoi(e);
+        c->src_tile = v == 16 || v == 32 ? v : kTile;
+    }
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
@@ -1307,7 +1316,7 @@ int gicp_set_source(gicp_ctx* c, const double* xyz, int64_t N, int dim, const gi
         if (nshards < 1 || shard < 0 || shard >= nshards) throw Fail{GICP_E_INVALID, "bad shard / nshards"};
         c->psrc = resolve(dim, p);
         c->top_ready = false;
-        build_cloud(c->src, xyz, N, dim, c->psrc, false, c->bs, c->stream, false, shard, nshards);
+        build_cloud(c->src, xyz, N, dim, c->psrc, false, c->bs, c->stream, false, shard, nshards, c->src_tile);
         set_shard(c, shard, nshards);
         HIPCHK(hipStreamSynchronize(c->stream));
     });
