@@ -37,6 +37,7 @@ hipError_t launch_knn_cov(const CovArgs&, int, int, bool, hipStream_t);
 hipError_t launch_corr(const CorrArgs&, int, int, hipStream_t);
 hipError_t launch_solve(IterState*, int, hipStream_t, double*);
 hipError_t launch_peer_probe(const PeerArgs&, double*, hipStream_t);
+hipError_t launch_reset_tiles(int32_t*, int32_t*, float*, int32_t*, int, int32_t*, int64_t, hipStream_t);
 hipError_t launch_graph_pack(const GraphArgs&, hipStream_t);
 hipError_t launch_rotate_cov(const double4*, const int32_t*, int64_t, int, const double*, double*, hipStream_t);
 hipError_t launch_top_weights(const double*, const int64_t*, const int32_t*, int64_t, int, double*, int64_t*, int, double*, int64_t*,
@@ -800,12 +801,10 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
 void reset_tile_state(gicp_ctx* c) {
     const int nt = std::max(1, c->src.ntiles);
     if (!c->d_hint) return;
-    HIPCHK(hipMemsetAsync(c->d_hint, 0xFF, sizeof(int32_t) * nt, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_list_len, 0, sizeof(int32_t) * nt, c->stream));
-    HIPCHK(hipMemsetAsync(c->d_list_rcert, 0, sizeof(float) * nt, c->stream));
-    if (c->d_cert_pass) HIPCHK(hipMemsetAsync(c->d_cert_pass, 0xFF, sizeof(int32_t) * nt, c->stream));
-    // last matches (k_corr's per-lane search cap): none yet
-    if (c->d_cert_j) HIPCHK(hipMemsetAsync(c->d_cert_j, 0xFF, sizeof(int32_t) * std::max<int64_t>(1, c->src.n), c->stream));
+    // hints -1, lists empty, certificates none (cert_pass -1) and no last match (cert_j -1: k_corr's per-lane
+    // search cap) -- one launch (five memsets were five queue operations, ~40 us of a C5 frame)
+    HIPCHK(launch_reset_tiles(c->d_hint, c->d_list_len, c->d_list_rcert, c->d_cert_pass, nt, c->d_cert_j,
+                              c->d_cert_j ? std::max<int64_t>(1, c->src.n) : 0, c->stream));
     c->pass = 0;
 }
 
@@ -1331,8 +1330,7 @@ int gicp_target_to_source(gicp_ctx* c, int shard, int nshards) {
         c->tgt.n = 0;
         c->tgt.cov_ready = false;
         c->psrc = c->ptgt;
-        set_shard(c, shard, nshards);
-        HIPCHK(hipStreamSynchronize(c->stream));
+        set_shard(c, shard, nshards);   // (its resets are stream-ordered before the next registration: no host sync)
     });
 }
 
@@ -1493,8 +1491,7 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
         hs.prev_mse = INFINITY;
         hs.pairs_total = 0.0;
         hs.converged_at = -1;
-        HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemsetAsync(&c->d_state->xchg_sum, 0, 3 * sizeof(double), st));   // this call's exchange timing
+        HIPCHK(hipMemcpyAsync(c->d_state, &hs, offsetof(IterState, stats), hipMemcpyHostToDevice, st));   // (xchg_* = 0)
         const int grid = corr_grid(c->src.ntiles, c->shard, c->nshards);
         const bool timing = res != nullptr && prm.timing_stride >= 0;   // < 0: no timing events
         const auto t0 = std::chrono::steady_clock::now();
@@ -1791,8 +1788,7 @@ int gicp_commit_target(gicp_ctx* c, int shard, int nshards) {
         g.cl.graph_ready = false;
         c->ptgt = g.p;
         c->top_ready = false;
-        if (c->src.n) set_shard(c, shard, nshards);
-        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->src.n) set_shard(c, shard, nshards);   // (stream-ordered resets: no host sync)
     });
 }
 

@@ -164,10 +164,11 @@ struct IterState {
     double prev_mse;          // +inf before the first pass
     double mse;               // mean squared correspondence distance of the last solved pass
     double pairs_total;       // distance pairs screened, summed over the passes k_solve consumed
+    // peer exchange timing (diagnostic, wall-clock ticks of the final workgroup's exchange, this call): in the
+    // header, so the host's one upload of the header at the start of a call also clears them
+    double xchg_sum, xchg_min, xchg_n;
     double stats[80];         // statistics of the last pass (summed over ranks when a communicator is set)
     double stats_solved[80];  // copy of the statistics the last k_solve consumed (reporting)
-    // peer exchange timing (diagnostic, wall-clock ticks of the final workgroup's exchange, this call)
-    double xchg_sum, xchg_min, xchg_n;
 };
 
 constexpr int kGroupWG = 64;       // workgroups per first-level reduction group

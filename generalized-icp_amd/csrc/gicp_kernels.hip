@@ -2711,6 +2711,28 @@ hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 
+// reset_tile_state's per-source-tile and per-point resets in one launch
+__global__ void __launch_bounds__(256) k_reset_tiles(int32_t* hint, int32_t* list_len, float* list_rcert,
+                                                     int32_t* cert_pass, int nt, int32_t* cert_j, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nt) {
+        hint[i] = -1;
+        list_len[i] = 0;
+        list_rcert[i] = 0.f;
+        if (cert_pass) cert_pass[i] = -1;
+    }
+    if (i < n) cert_j[i] = -1;
+}
+
+hipError_t launch_reset_tiles(int32_t* hint, int32_t* list_len, float* list_rcert, int32_t* cert_pass, int nt,
+                              int32_t* cert_j, int64_t n, hipStream_t st) {
+    const int64_t m = std::max<int64_t>(nt, n);
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reset_tiles, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, hint, list_len, list_rcert,
+                       cert_pass, nt, cert_j, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_peer_probe(const PeerArgs& p, double* out, hipStream_t st) {
     hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, st, p, kPeerProbeRounds, out);
     return hipGetLastError();
