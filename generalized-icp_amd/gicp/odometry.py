@@ -43,9 +43,10 @@ class Odometry:
     def reset(self):
         """Start a new stream (the device context and its buffers are kept)."""
         dim = self.dim
-        self.pose = np.eye(dim + 1)          # current sensor -> world (first frame = origin)
-        self.poses = [self.pose.copy()]
-        self.yaw_xy = (0.0, 0.0, 0.0)        # reference-formula state (x, y, yaw)
+        self._pose = np.eye(dim + 1)         # current sensor -> world (first frame = origin)
+        self._poses = [self._pose.copy()]
+        self._yaw_xy = (0.0, 0.0, 0.0)       # reference-formula state (x, y, yaw)
+        self._pending = []                   # registrations not yet composed into the pose (see _flush)
         self.last_T = None
         self.frames = 0
         if getattr(self, "_staged", None):
@@ -118,8 +119,33 @@ class Odometry:
             yield self.step(cur, next_scans=window[:depth])
 
     def _integrate(self, T):
-        self.pose, self.yaw_xy = compose(self.pose, T, self.composition, self.yaw_xy)
-        self.poses.append(self.pose.copy())
+        # composed when the pose is read (the same compositions in the same order): the stream's loop does not
+        # wait on a 4 x 4 inverse per frame
+        self._pending.append(T)
+
+    def _flush(self):
+        for T in self._pending:
+            self._pose, self._yaw_xy = compose(self._pose, T, self.composition, self._yaw_xy)
+            self._poses.append(self._pose.copy())
+        self._pending = []
+
+    @property
+    def pose(self):
+        """Current sensor -> world pose."""
+        self._flush()
+        return self._pose
+
+    @property
+    def poses(self):
+        """Sensor poses of every frame so far (the first frame is the origin)."""
+        self._flush()
+        return self._poses
+
+    @property
+    def yaw_xy(self):
+        """The reference formula's planar state (x, y, yaw) (composition='reference')."""
+        self._flush()
+        return self._yaw_xy
 
 
 def compose(pose, T, composition="se3", yaw_xy=(0.0, 0.0, 0.0)):
