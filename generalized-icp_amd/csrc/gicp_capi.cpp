@@ -602,7 +602,7 @@ int shard_tile_count(int ntiles, int shard, int nshards) {
 // cov_shard / cov_nshards: the covariances are computed for that shard's tiles only (a sharded source: every
 // rank needs the whole cloud's index for the neighbourhoods, but only its own tiles' covariances); the other
 // rows read NaN.
-// tile_points: points per tile at most (64; a source may take 32 or 16, CorrArgs / DESIGN.md §3h)
+// tile_points: points per tile at most (64; a source may take 32 or 16: GICP_SRC_TILE)
 void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_params& p, bool graph,
                  BuildScratch& bs, hipStream_t st, bool staged = false, int cov_shard = 0, int cov_nshards = 1,
                  int tile_points = kTile) {
