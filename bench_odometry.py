@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--fixed", action="store_true", help="fixed iterations (convergence disabled)")
     ap.add_argument("--tolerance", type=float, default=1e-6)
     ap.add_argument("--sync", action="store_true", help="build each scan when needed (no staged double buffer)")
+    ap.add_argument("--kernel-times", action="store_true", help="keep the library's sampled per-launch HIP events")
     ap.add_argument("--copy", action="store_true",
                     help="staged scans copied by the library before stage_target returns (the default for callers "
                          "that refill their buffer); without it the bench, which holds every frame untouched in "
@@ -49,6 +50,10 @@ def main():
     import gicp
     p = gicp.default_params(3, max_iterations=a.max_iterations, tolerance=a.tolerance,
                             fixed_iterations=1 if a.fixed else 0, **kw)
+    if not a.kernel_times:
+        # no per-launch HIP event pairs (a diagnostic the line does not report: each pair is queue work between
+        # two launches); --kernel-times keeps the library default (every 8th launch timed)
+        p.timing_stride = -1
     odo = Odometry(3, params=p, borrow=not a.copy)
     # warm-up on the first two frames (library init, allocation), then restart the stream
     odo.step(frames[0][0])
