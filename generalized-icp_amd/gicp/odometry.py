@@ -135,6 +135,11 @@ class Odometry:
         self._flush()
         return self._pose
 
+    @pose.setter
+    def pose(self, value):   # (e.g. a stream that starts from a known sensor pose)
+        self._flush()
+        self._pose = np.asarray(value, dtype=np.float64).copy()
+
     @property
     def poses(self):
         """Sensor poses of every frame so far (the first frame is the origin)."""
