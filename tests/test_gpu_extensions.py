@@ -323,3 +323,31 @@ def test_native_library_built_from_these_sources(eng):
     assert info["src"] == _lib.source_hash(), info
     assert os.path.dirname(_lib.LIB_PATH) == os.path.dirname(os.path.abspath(gicp.__file__))
     print(f"gicp_build_info: {info}")
+
+
+@pytest.mark.parametrize("tile", ["32", "16"])
+def test_smaller_source_tiles_same_correspondences(monkeypatch, scene3d, tile):
+    """GICP_SRC_TILE (source tiles of at most 32 / 16 points): the same exact nearest neighbours
+    as the oracle's KD-tree (indices bit-exact), statistics within 1e-11 of the 64-point tiling's (the per-unit
+    partial sums group the points differently), and the same registration to 1e-9."""
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, fixed_iterations=1, max_iterations=8, **P3)
+    T = _pose()
+    moved = O.apply_transformation(src, T)
+    idx, _ = O.correspondences(moved, tgt, P3["max_distance_correspondence"])
+    out = {}
+    for t in ("64", tile):
+        monkeypatch.setenv("GICP_SRC_TILE", t)
+        e = gicp.Engine(0)
+        try:
+            e.set_target(tgt, p)
+            e.set_source(src, p)
+            st, dbg = e.iterate(T, debug=True)
+            Tr, _ = e.align(None, p)
+        finally:
+            e.close()
+        out[t] = (st, dbg["index"], Tr)
+    assert np.array_equal(out[tile][1], idx)
+    ref = out["64"][0]
+    np.testing.assert_allclose(out[tile][0], ref, rtol=1e-11, atol=1e-11 * np.max(np.abs(ref)))
+    np.testing.assert_allclose(out[tile][2], out["64"][2], rtol=0, atol=1e-9)
