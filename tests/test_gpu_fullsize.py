@@ -170,6 +170,28 @@ def test_2d_100k_fast_mode_vs_oracle(eng):
         assert abs(th) < 1e-6 and np.max(np.abs(a[:2, 2] - b[:2, 2])) < 1e-4, (th, a, b)   # px, box 1000
 
 
+def test_2d_1m_fast_mode_vs_oracle(eng):
+    """The 2-D bench size (BASELINE.md §3's segment scene at 1M/1M, k = 6): the first pass's 1M correspondence
+    indices bit-exact against cKDTree, and 5 fixed iterations of the fast path within 1e-8 rad / 1e-6 px of
+    the oracle's loop with the same semantics (rotated covariances, exact inner solve) at every iteration."""
+    src, tgt, _ = S.segment_scene_2d(1_000_000)
+    kw = dict(max_distance_correspondence=20.0, max_distance_nearest_neighbors=25.0)
+    p = gicp.default_params(2, **kw)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    _, dbg = eng.iterate(np.eye(3), debug=True)
+    idx, _ = O.correspondences(src, tgt, kw["max_distance_correspondence"], workers=WORKERS)
+    assert np.array_equal(dbg["index"], idx)
+    T, all_T, *_ = gicp.gicp(src, tgt, max_iterations=5, tolerance=0.0, mode="fast", inner="newton",
+                             full_output=False, verbose=False, **kw)
+    To, all_To, *_ = O.gicp(src, tgt, max_iterations=5, tolerance=0.0, inner="gn", source_cov="rotate",
+                            fixed_iterations=True, workers=WORKERS, **kw)
+    assert len(all_T) == len(all_To) == 6
+    for a, b in zip(all_T, all_To):
+        th = np.arctan2(a[1, 0], a[0, 0]) - np.arctan2(b[1, 0], b[0, 0])
+        assert abs(th) < 1e-8 and np.max(np.abs(a[:2, 2] - b[:2, 2])) < 1e-6, (th, a, b)
+
+
 def test_2d_default_above_faithful_limit_vs_oracle():
     """a 2-D call just above FAITHFUL_MAX_POINTS takes mode='fast' (rotated covariances,
     fmin_cg on the closed-form loss); its endpoint is within the parity tolerance (1e-4 rad, 1e-3 px)
