@@ -175,7 +175,10 @@ constexpr int kGroupWG = 64;       // workgroups per first-level reduction group
 // grids of at most this many units reduce in one level: the final workgroup sums every unit's partial itself
 // (its loads cover 81 units per round trip, k_corr sum_rows), one ticket and one round trip of stores fewer;
 // beyond it the one ticket's queue (every unit on one counter) and a third round trip of loads cost more
-constexpr int kFlatUnits = 128;
+#ifndef GICP_FLAT_UNITS
+#define GICP_FLAT_UNITS 128
+#endif
+constexpr int kFlatUnits = GICP_FLAT_UNITS;
 // Source shards are interleaved in chunks of kShardChunk units (a unit = kCorrWaves source tiles,
 // one k_corr workgroup): rank r of G reduces global chunks r, r + G, r + 2G, ...  Contiguous Morton
 // ranges left the ranks unbalanced (the registration's far walls are the heavy tiles: one rank of 8
