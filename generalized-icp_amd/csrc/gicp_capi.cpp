@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -408,6 +409,8 @@ struct gicp_ctx {
     int64_t* d_trace_top = nullptr;   // [iter][16] source, then [iter][16] target
     double* d_trace_det = nullptr;    // [iter][16]
     size_t cap_ttop = 0, cap_tdet = 0;
+    unsigned long long* d_tail = nullptr;   // GICP_TAIL diagnostic build: [iter][kTailWords] (on this context's device)
+    size_t cap_tail = 0;
     static constexpr int kMaxBatch = 64;
     hipEvent_t ev[2 * kMaxBatch] = {};
     int batch_hint = 0;               // iterations the last converging align ran: its first batch next time
@@ -1237,6 +1240,7 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_hist);
     dfree(c->d_trace_top);
     dfree(c->d_trace_det);
+    dfree(c->d_tail);
     for (auto& e : c->ev)
         if (e) quiet(hipEventDestroy(e));
     if (c->stream) quiet(hipStreamDestroy(c->stream));
@@ -1505,19 +1509,17 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
 #ifdef GICP_TAIL
         // diagnostic build: one tail record per iteration (gicp_internal.h kTailWords), dumped raw to
         // $GICP_TAIL_DUMP.<call> after the loop
-        static unsigned long long* d_tail = nullptr;
-        static size_t tail_cap = 0;
-        static int tail_seq = 0;
+        static std::atomic<int> tail_seq{0};   // dump file counter (process-wide)
         const char* tail_path = std::getenv("GICP_TAIL_DUMP");
         const size_t ntail = (size_t)std::max(1, prm.max_iterations) * kTailWords;
-        if (tail_path) {
-            if (ntail > tail_cap) {
-                dalloc(d_tail, ntail);
-                tail_cap = ntail;
-            }
+        unsigned long long* d_tail = nullptr;
+        if (tail_path) {   // the context's own buffer, on its device
+            dreserve(c->d_tail, c->cap_tail, ntail);
+            d_tail = c->d_tail;
             std::vector<unsigned long long> init(ntail, 0ull);
             for (size_t k = 0; k < ntail; k += kTailWords) init[k] = ~0ull;
-            HIPCHK(hipMemcpy(d_tail, init.data(), ntail * 8, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpyAsync(d_tail, init.data(), ntail * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
         }
 #endif
         // Iterations are enqueued in batches with no host sync inside a batch: each is k_corr (pose
@@ -1597,7 +1599,8 @@ int gicp_align_trace(gicp_ctx* c, const double* T0, const gicp_params* p, double
 #ifdef GICP_TAIL
         if (tail_path) {
             std::vector<unsigned long long> h(ntail);
-            HIPCHK(hipMemcpy(h.data(), d_tail, ntail * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpyAsync(h.data(), d_tail, ntail * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
             const std::string path = std::string(tail_path) + "." + std::to_string(tail_seq++);
             if (FILE* fp = std::fopen(path.c_str(), "wb")) {
                 std::fwrite(h.data(), 8, h.size(), fp);

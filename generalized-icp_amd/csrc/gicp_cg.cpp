@@ -16,6 +16,33 @@
 // (OpenBLAS ddot; checked against numpy in tests/test_cg_native.py), so dot() below is one too; every
 // other operation is the elementwise IEEE operation NumPy performs.  tests/test_cg_native.py pins the result
 // bit for bit against scipy's fmin_cg run on the same closed form.
+//
+// The algorithm, control flow and constants below are derived from SciPy, whose licence follows:
+//
+//   Copyright (c) 2001-2002 Enthought, Inc. 2003, SciPy Developers.
+//   All rights reserved.
+//
+//   Redistribution and use in source and binary forms, with or without modification, are permitted provided
+//   that the following conditions are met:
+//
+//   1. Redistributions of source code must retain the above copyright notice, this list of conditions and the
+//      following disclaimer.
+//   2. Redistributions in binary form must reproduce the above copyright notice, this list of conditions and
+//      the following disclaimer in the documentation and/or other materials provided with the distribution.
+//   3. Neither the name of the copyright holder nor the names of its contributors may be used to endorse or
+//      promote products derived from this software without specific prior written permission.
+//
+//   THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND CONTRIBUTORS "AS IS" AND ANY EXPRESS OR IMPLIED
+//   WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR A
+//   PARTICULAR PURPOSE ARE DISCLAIMED. IN NO EVENT SHALL THE COPYRIGHT HOLDER OR CONTRIBUTORS BE LIABLE FOR ANY
+//   DIRECT, INDIRECT, INCIDENTAL, SPECIAL, EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO,
+//   PROCUREMENT OF SUBSTITUTE GOODS OR SERVICES; LOSS OF USE, DATA, OR PROFITS; OR BUSINESS INTERRUPTION)
+//   HOWEVER CAUSED AND ON ANY THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING
+//   NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS SOFTWARE, EVEN IF ADVISED OF THE
+//   POSSIBILITY OF SUCH DAMAGE.
+//
+// The line search follows SciPy's _dcsrch.py, SciPy's translation of MINPACK-2's dcsrch / dcstep
+// (J. J. Moré and D. J. Thuente, Argonne National Laboratory and University of Minnesota).
 #pragma clang fp contract(off)
 
 #include <cmath>

@@ -276,9 +276,10 @@ struct CorrArgs {
 };
 // GICP_TAIL record of one k_corr launch: [0] workgroup 0's start, [1] the final workgroup's partial stored,
 // then the final workgroup: [2] its group ticket won, [3] group sum stored, [4] final ticket won, [5] final
-// sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] why lanes walked
-// (counts, k_corr: no last match / descent local minimum without proof / uncovered near tie / hops exhausted /
-// walking lanes / walking waves / waves with one walking lane)
+// sum in LDS, [6] peer exchange done, [7] statistics stored, [8] solve done; [9..15] how lanes' searches
+// ended (counts over the launch): [9] lanes that descended the target graph, [10..13] lanes the descent proved
+// at the start node's local minimum / at a row entry of the start node / after a hop / by an exactly resolved
+// near tie, [14] walking lanes, [15] walking waves
 constexpr int kTailWords = 16;
 
 constexpr int nstat(int D) {

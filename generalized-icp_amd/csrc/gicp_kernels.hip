@@ -114,12 +114,16 @@ struct Stamps {
     // 5 traversal block tests, 6 traversal candidate blocks, 7 fp64 fallback tiles
     unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     __device__ __forceinline__ void count(int k, unsigned v = 1) { cnt[k] += v; }
-#elif defined(GICP_TIMELINE)   // `make VARIANT=tl VDEFS=-DGICP_TIMELINE`: wave start/end only
+#elif defined(GICP_TIMELINE)   // `make VARIANT=tl VDEFS=-DGICP_TIMELINE`: wave start/end, phase ends, counters
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // realtime (100 MHz) at the end of the certificate + descent phase and at the end of the walk; the walk's
+    // kind (0 none, 1 candidate list, 2 list then full walk, 3 full walk); lanes that descended / walked
+    unsigned long long tdesc = 0, twalk = 0;
+    unsigned kind = 0, ndesc = 0, nwalk = 0;
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
-    __device__ __forceinline__ void count(int, unsigned = 1) {}
+    __device__ __forceinline__ void count(int k, unsigned v = 1) { cnt[k] += v; }
 #else
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
@@ -1737,11 +1741,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         const bool any_gcert = wave_any(gcert);
         const bool skip_walk = !wave_any(q.valid && !cert);
 #ifdef GICP_TAIL
-        if (A.tail) {   // why lanes walk: [9] no last match, [10] descent at a local minimum without proof,
-                        // [11] a near tie the row does not cover, [12] hops exhausted, [13] walking lanes,
-                        // [14] walking waves, [15] walking waves with one walking lane (per-wave counts into the
-                        // workgroup's LDS, one global add per workgroup at its end)
-            // [9] lanes that descended, [10..13] proved by gout 1..4, [14] walking lanes, [15] walking waves
+        if (A.tail) {   // how searches ended (per-wave counts into the workgroup's LDS, one global add per
+                        // workgroup at its end): [9] lanes that descended, [10..13] proved by gout 1..4,
+                        // [14] walking lanes, [15] walking waves
             const bool wl = q.valid && !cert;
             const uint64_t wm = __ballot(wl);
             const int cd = __popcll(__ballot(have_jp));
@@ -1759,6 +1761,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #endif
         ngproved = __popcll(__ballot(gcert));
         nwalked = skip_walk ? 0 : 1;
+#ifdef GICP_TIMELINE
+        S.tdesc = __builtin_amdgcn_s_memrealtime();
+        S.ndesc = (unsigned)__popcll(__ballot(have_jp));
+        S.nwalk = (unsigned)__popcll(__ballot(q.valid && !cert));
+#endif
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
         // farther than kappa since its last pass (the pose is still converging) walks without it
         const float kap = cdelta > A.kappa ? 0.f : A.kappa;
@@ -1932,6 +1939,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
         }
         S.mark(1);
+#ifdef GICP_TIMELINE
+        S.twalk = __builtin_amdgcn_s_memrealtime();
+        S.kind = skip_walk ? 0u : use ? 1u : list_rebuilds > 0 ? 2u : 3u;
+#endif
 
         // the fp64 source point is needed only from here on (kept out of the walk's registers).  A wave
         // that walked needs it now (fp64 fallback); one that skipped the walk requests it with its
@@ -2271,6 +2282,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         o[0] = (unsigned)T;                              // the wave's source tile, its radius and size
         o[1] = __float_as_uint(st.radius);
         o[2] = (unsigned)st.count;
+        o[3] = S.tdesc;                                  // certificates + descent done (0: the wave had no tile)
+        o[4] = S.twalk;                                  // walk done
+        o[5] = S.kind | (S.ndesc << 8) | (S.nwalk << 16);
+        o[6] = (unsigned)pairs;
+        o[7] = (unsigned)namb_total;
+        for (int c = 0; c < 8; ++c) o[8 + c] = S.cnt[c];
 #endif
         o[17] = __builtin_amdgcn_s_memrealtime();
         o[18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
@@ -2584,9 +2601,15 @@ __global__ void __launch_bounds__(256) k_top2(const double* pv, const int64_t* p
     }
 }
 
+// Each launcher reports hipGetLastError() after its launches.  HIP's last error is per thread and shared
+// with every other HIP user on it (torch, RCCL, the caller): one such user's failed call left there must not
+// fail this library's launch check, so each launcher clears it first.
+static inline void clear_foreign_error() { (void)hipGetLastError(); }
+
 hipError_t launch_top_weights(const double* det, const int64_t* tgt_sorted, const int32_t* perm, int64_t n, int k,
                               double* scratch_v, int64_t* scratch_i, int blocks, double* ov, int64_t* osrc,
                               int64_t* otgt, hipStream_t st) {
+    clear_foreign_error();
     if (k < 1 || k > kTopMax || blocks < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_top1, dim3(blocks), dim3(256), 0, st, det, perm, n, k, scratch_v, scratch_i);
     hipLaunchKernelGGL(k_top2, dim3(1), dim3(256), 0, st, scratch_v, scratch_i, blocks * k, k, tgt_sorted, ov, osrc,
@@ -2629,6 +2652,7 @@ __global__ void __launch_bounds__(256) k_rotate_cov(const double4* __restrict__ 
 // ---------------------------------------------------------------------------
 hipError_t launch_rotate_cov(const double4* cov, const int32_t* perm, int64_t n, int dim, const double* R, double* out,
                              hipStream_t st) {
+    clear_foreign_error();
     if (n <= 0) return hipSuccess;
     Rot r{};
     for (int k = 0; k < dim * dim; ++k) r.r[k] = R[k];
@@ -2640,6 +2664,7 @@ hipError_t launch_rotate_cov(const double4* cov, const int32_t* perm, int64_t n,
 
 hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& fr, uint32_t* codes, int32_t* idx,
                          hipStream_t st) {
+    clear_foreign_error();
     const int bs = 256;
     const unsigned g = (unsigned)((n + bs - 1) / bs);
     hipLaunchKernelGGL(k_morton, dim3(g), dim3(bs), 0, st, xyz, n, dim, fr, codes, idx);
@@ -2649,6 +2674,7 @@ hipError_t launch_morton(const double* xyz, int64_t n, int dim, const DevCloud& 
 hipError_t launch_build_tiles(const double* xyz_in, int dim, int32_t* perm, TileInfo* tiles, TileBox* boxes,
                               int ntiles, double* xyz64, float4* rel32, int32_t* inv, unsigned* rho_bits,
                               hipStream_t st) {
+    clear_foreign_error();
     const unsigned g = (unsigned)((ntiles + kWavesPerWG - 1) / kWavesPerWG);
     hipLaunchKernelGGL(k_build_tiles, dim3(g), dim3(256), 0, st, xyz_in, dim, perm, tiles, boxes, ntiles, xyz64,
                        rel32, inv, rho_bits);
@@ -2657,6 +2683,7 @@ hipError_t launch_build_tiles(const double* xyz_in, int dim, int32_t* perm, Tile
 
 hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blocks, int nblocks, int dim,
                                hipStream_t st) {
+    clear_foreign_error();
     const unsigned g = (unsigned)((nblocks + kWavesPerWG - 1) / kWavesPerWG);
     hipLaunchKernelGGL(k_build_blocks<TileInfo>, dim3(g), dim3(256), 0, st, tiles, ntiles, blocks, nblocks, dim);
     const int nsuper = (nblocks + kBlockTiles - 1) / kBlockTiles;   // super-blocks at blocks[nblocks..]
@@ -2667,6 +2694,7 @@ hipError_t launch_build_blocks(const TileInfo* tiles, int ntiles, BlockInfo* blo
 }
 
 hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, bool graph, hipStream_t st) {
+    clear_foreign_error();
     const int nq = a.q_end - a.q_begin;
     if (nq <= 0) return hipSuccess;
     if (a.split != 1 && a.split != kSub) return hipErrorInvalidValue;
@@ -2686,6 +2714,7 @@ hipError_t launch_knn_cov(const CovArgs& a, int dim, int k, bool graph, hipStrea
 }
 
 hipError_t launch_graph_pack(const GraphArgs& a, hipStream_t st) {
+    clear_foreign_error();
     if (a.cl.n <= 0) return hipSuccess;
     const unsigned gp = (unsigned)((a.cl.n + 255) / 256);
     hipLaunchKernelGGL(k_graph_pack, dim3(gp), dim3(256), 0, st, a.nb, a.nbh, a.cl.n, a.nbq, a.nbi);
@@ -2705,6 +2734,7 @@ int corr_grid(int q_tiles, int shard, int nshards) {
 }
 
 hipError_t launch_corr(const CorrArgs& a, int dim, int grid, hipStream_t st) {
+    clear_foreign_error();
     if (grid <= 0) return hipSuccess;
     if (dim == 2) hipLaunchKernelGGL(k_corr<2>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
     else hipLaunchKernelGGL(k_corr<3>, dim3(grid), dim3(64 * kCorrWaves), 0, st, a);
@@ -2726,6 +2756,7 @@ __global__ void __launch_bounds__(256) k_reset_tiles(int32_t* hint, int32_t* lis
 
 hipError_t launch_reset_tiles(int32_t* hint, int32_t* list_len, float* list_rcert, int32_t* cert_pass, int nt,
                               int32_t* cert_j, int64_t n, hipStream_t st) {
+    clear_foreign_error();
     const int64_t m = std::max<int64_t>(nt, n);
     if (m <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_reset_tiles, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, hint, list_len, list_rcert,
@@ -2734,11 +2765,13 @@ hipError_t launch_reset_tiles(int32_t* hint, int32_t* list_len, float* list_rcer
 }
 
 hipError_t launch_peer_probe(const PeerArgs& p, double* out, hipStream_t st) {
+    clear_foreign_error();
     hipLaunchKernelGGL(k_peer_probe, dim3(1), dim3(64), 0, st, p, kPeerProbeRounds, out);
     return hipGetLastError();
 }
 
 hipError_t launch_solve(IterState* st, int dim, hipStream_t stream, double* hist) {
+    clear_foreign_error();
     if (dim == 2) hipLaunchKernelGGL(k_solve<2>, dim3(1), dim3(64), 0, stream, st, hist);
     else hipLaunchKernelGGL(k_solve<3>, dim3(1), dim3(64), 0, stream, st, hist);
     return hipGetLastError();

@@ -607,7 +607,9 @@ def gicp(source_points, target_points, max_iterations=100, tolerance=1e-6, max_d
       statistics in one pass, and the inner problem is solved from them -- exactly by
       Newton on SO(d) (inner='newton', the 3-D default: the whole loop then runs on the
       device in one gicp_align_trace call, the 7-tuple's per-iteration rows recorded there),
-      or by scipy's fmin_cg on the closed form (inner='cg', the 2-D default, host loop).
+      or by conjugate gradients on the closed form (inner='cg', the 2-D default, host loop): the
+      native gicp_cg_inner_2d, a C++ restatement of SciPy 1.15.3's fmin_cg pinned bit for bit
+      against scipy's own on the same closed form (tests/test_cg_native.py).
     full_output=False skips the per-point visualisation extras (the three
     lists come back empty), which is what large clouds want.  In 'fast' mode the
     top-5 det(W) points are selected on the GPU (no per-point copy) and

@@ -61,8 +61,10 @@ class Odometry:
         """Add one scan; returns (T, result) of its registration against the previous scan, or
         (None, None) for the first frame.  `next_scan` (or the list `next_scans`, at most
         Engine.MAX_STAGED), if given, is built on the device while this pair is registered; pass the
-        same objects as `scan` of the next calls, in order (the library copies a staged scan before
-        the call returns: the caller may reuse the array)."""
+        same objects as `scan` of the next calls, in order.  By default the library copies a staged scan
+        before the call returns, so the caller may reuse the array at once; with borrow=True the library
+        reads the caller's array in place (no copy on this thread), and the caller must leave it unchanged
+        until that scan has itself been step()ped."""
         t0 = time.perf_counter()
         if self._staged and self._staged[0] is scan:
             try:
@@ -136,9 +138,18 @@ class Odometry:
         return self._pose
 
     @pose.setter
-    def pose(self, value):   # (e.g. a stream that starts from a known sensor pose)
+    def pose(self, value):
+        """Set the current sensor pose (e.g. a stream that starts from a known pose).  It replaces the
+        latest entry of `poses`, and the reference formula's planar state follows it (x, y and the yaw of
+        the pose's first two axes), so either composition continues from it."""
         self._flush()
-        self._pose = np.asarray(value, dtype=np.float64).copy()
+        P = np.asarray(value, dtype=np.float64).copy()
+        d = self.dim
+        if P.shape != (d + 1, d + 1):
+            raise ValueError(f"pose must be {d + 1} x {d + 1}")
+        self._pose = P
+        self._poses[-1] = P.copy()
+        self._yaw_xy = (float(P[0, d]), float(P[1, d]), math.atan2(P[1, 0], P[0, 0]))
 
     @property
     def poses(self):
@@ -146,11 +157,30 @@ class Odometry:
         self._flush()
         return self._poses
 
+    @poses.setter
+    def poses(self, value):
+        self._flush()
+        self._poses = [np.asarray(P, dtype=np.float64).copy() for P in value]
+
     @property
     def yaw_xy(self):
         """The reference formula's planar state (x, y, yaw) (composition='reference')."""
         self._flush()
         return self._yaw_xy
+
+    @yaw_xy.setter
+    def yaw_xy(self, value):
+        """Set the planar state; with composition='reference' the pose is rebuilt from it, as compose does."""
+        self._flush()
+        x, y, yaw = (float(v) for v in value)
+        self._yaw_xy = (x, y, yaw)
+        if self.composition == "reference":
+            d = self.dim
+            P = np.eye(d + 1)
+            c, s = math.cos(yaw), math.sin(yaw)
+            P[0, 0], P[0, 1], P[1, 0], P[1, 1] = c, -s, s, c
+            P[0, d], P[1, d] = x, y
+            self._pose = P
 
 
 def compose(pose, T, composition="se3", yaw_xy=(0.0, 0.0, 0.0)):

@@ -1,0 +1,114 @@
+"""Which waves end each pass of the driver's registration (attribute the long pole).
+
+    make -C generalized-icp_amd/csrc VARIANT=tl VDEFS=-DGICP_TIMELINE
+    GICP_LIB_VARIANT=tl python scripts/last_waves.py [--n 1000000] [--passes 20] [--shard-sim 1]
+
+The bench's clouds, a cold registration from the identity: pass k runs at the pose the solve of pass k-1 gave
+(gicp_iterate + the host solve, the sequence gicp_align runs), each launch's per-wave record dumped by the
+timeline build (gicp_kernels.hip GICP_TIMELINE: wave start and end, the end of its certificate + descent
+phase, the end of its walk, the walk's kind, lanes that descended / walked, tile visits, tiles scanned, list
+use, block tests).  Per pass it prints the span and, for the last 1 % of waves to finish (and the last 10),
+what they did: the phase that took their time, the walk's kind, visits, walking lanes, start time.
+"""
+import argparse
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "generalized-icp_amd"), ROOT]
+
+KIND = {0: "none", 1: "list", 2: "list+full", 3: "full"}
+
+
+def waves(path):
+    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 20).astype(np.int64)
+    live = a[:, 17] > 0
+    a = a[live]
+    t0 = a[:, 16]
+    base = t0.min()
+    us = lambda x: (x - base) / 100.0   # noqa: E731  (100 MHz realtime)
+    has_tile = a[:, 3] > 0
+    w = dict(
+        tile=a[:, 0], start=us(a[:, 16]), end=us(a[:, 17]),
+        desc_end=np.where(has_tile, us(a[:, 3]), us(a[:, 16])),
+        walk_end=np.where(has_tile, us(a[:, 4]), us(a[:, 16])),
+        kind=a[:, 5] & 0xFF, ndesc=(a[:, 5] >> 8) & 0xFF, nwalk=(a[:, 5] >> 16) & 0xFF,
+        pairs=a[:, 6], amb=a[:, 7], visits=a[:, 8], scanned=a[:, 9], list_used=a[:, 11], blk=a[:, 13],
+        fb=a[:, 15], xcc=a[:, 19] & 7)
+    w["t_desc"] = w["desc_end"] - w["start"]
+    w["t_walk"] = w["walk_end"] - w["desc_end"]
+    w["t_epi"] = w["end"] - w["walk_end"]
+    return w
+
+
+def describe(w, sel, label):
+    k = np.bincount(w["kind"][sel], minlength=4)
+    phase = np.argmax(np.stack([w["t_desc"][sel], w["t_walk"][sel], w["t_epi"][sel]]), axis=0)
+    ph = np.bincount(phase, minlength=3)
+    return (f"  {label:10s} n {sel.sum():5d}  start {np.mean(w['start'][sel]):6.1f}  dur {np.mean((w['end'] - w['start'])[sel]):6.1f}"
+            f"  [desc {np.mean(w['t_desc'][sel]):5.1f} walk {np.mean(w['t_walk'][sel]):5.1f} epi {np.mean(w['t_epi'][sel]):5.1f}]"
+            f"  longest phase d/w/e {ph[0]}/{ph[1]}/{ph[2]}  walk none/list/l+f/full {k[0]}/{k[1]}/{k[2]}/{k[3]}"
+            f"  visits {np.mean(w['visits'][sel]):5.1f}  walkers {np.mean(w['nwalk'][sel]):4.1f}  desc {np.mean(w['ndesc'][sel]):4.1f}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--passes", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--shard-sim", type=int, default=1)
+    a = ap.parse_args()
+    tmp = tempfile.mkdtemp(prefix="gicp_tl_")
+    os.environ["GICP_STAMPS_DUMP"] = os.path.join(tmp, "st")
+    import gicp
+    from gicp import _lib
+    from gicp import synthetic as S
+    assert _lib.LIB_PATH.endswith("libgicp_hip_tl.so"), "run with GICP_LIB_VARIANT=tl (the timeline build)"
+    src, tgt, _ = S.scene_pair_3d(a.n)
+    p = gicp.default_params(3, max_distance_correspondence=0.5, max_distance_nearest_neighbors=1.0)
+    e = gicp.Engine(0)
+    e.set_target(tgt, p)
+    e.set_source(src, p, shard=0, nshards=a.shard_sim)
+    T = np.eye(4)
+    for _ in range(a.warmup):   # as bench.py: a warmup registration, then the caches are dropped
+        st = e.iterate(T)
+        T, _ = gicp.solve_pose(st, T)
+    e.reset_cache()
+    first = len([f for f in os.listdir(tmp) if f.startswith("st.")])
+    T = np.eye(4)
+    for _ in range(a.passes):
+        st = e.iterate(T)
+        T, _ = gicp.solve_pose(st, T)
+    e.close()
+    print(f"n {a.n}  shard 1/{a.shard_sim}  passes {a.passes} (cold, from the identity; gicp_iterate + host solve)")
+    print("per pass: span of the waves (first start -> last end, us) and the waves ending it; phases: desc = prologue +"
+          " certificates + graph descent, walk = list / full walk + fp64 re-resolution start, epi = the rest")
+    for k in range(a.passes):
+        w = waves(os.path.join(tmp, f"st.{first + k}"))
+        end = w["end"]
+        span = end.max()
+        n1 = max(1, len(end) // 100)
+        order = np.argsort(-end)
+        last1 = np.zeros(len(end), bool)
+        last1[order[:n1]] = True
+        walkers = w["nwalk"] > 0
+        print(f"pass {k:2d}: span {span:6.1f} us  waves {len(end)}  walking waves {walkers.sum()}"
+              f" (<= 8 walkers: {(walkers & (w['nwalk'] <= 8)).sum()})  p50 end {np.median(end):6.1f}  p99 end {np.percentile(end, 99):6.1f}")
+        print(describe(w, np.ones(len(end), bool), "all"))
+        if walkers.any():
+            print(describe(w, walkers, "walking"))
+        print(describe(w, last1, "last 1%"))
+        for i in order[:6]:
+            print(f"    tile {w['tile'][i]:6d} xcc {w['xcc'][i]} start {w['start'][i]:6.1f} desc {w['t_desc'][i]:5.1f}"
+                  f" walk {w['t_walk'][i]:5.1f} ({KIND[int(w['kind'][i])]}, {w['visits'][i]} visits, {w['scanned'][i]} scanned,"
+                  f" {w['nwalk'][i]} walkers) epi {w['t_epi'][i]:5.1f} end {w['end'][i]:6.1f}")
+    for f in os.listdir(tmp):
+        os.remove(os.path.join(tmp, f))
+    os.rmdir(tmp)
+
+
+if __name__ == "__main__":
+    main()

@@ -430,3 +430,22 @@ def test_non_finite_input_is_rejected(eng):
     pts[17, 1] = np.inf
     with pytest.raises(ValueError):
         eng.set_source(pts, gicp.default_params(3))
+
+
+def test_foreign_hip_error_does_not_fail_the_next_call(eng, scene3d):
+    """HIP's last error is per thread and shared with every HIP user on it.  A failed call of
+    another user (here hipSetDevice on a device that does not exist, through the HIP runtime directly) left
+    on this thread must not make the library's next launch check report GICP_E_HIP."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0   # the foreign failure, left unread
+    src, tgt, _ = scene3d
+    p = gicp.default_params(3, max_iterations=3, fixed_iterations=1, **P3)
+    eng.set_target(tgt, p)
+    eng.set_source(src, p)
+    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0
+    T, res = eng.align(None, p)
+    assert res["iterations"] == 3 and np.all(np.isfinite(T))
+    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0
+    st = eng.iterate(np.eye(4))
+    assert st[-1] > 0

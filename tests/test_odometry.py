@@ -40,6 +40,35 @@ def test_compose_reference_formula():
         np.testing.assert_allclose(P, _planar(x, y, yaw), atol=1e-12)
 
 
+def _bare_odometry(composition, dim=2):
+    """An Odometry without a device context: pose bookkeeping (_integrate / pose / poses) never calls it."""
+    from gicp.odometry import Odometry
+    o = Odometry.__new__(Odometry)
+    o.dim, o.composition, o._staged = dim, composition, []
+    o.reset()
+    return o
+
+
+@pytest.mark.parametrize("composition", ["se3", "reference"])
+def test_pose_setter_continues_either_composition(composition):
+    """setting `pose` replaces the latest pose and the reference formula's planar state, so the
+    next registration composes from it under either composition."""
+    o = _bare_odometry(composition)
+    start = _planar(1.0, -2.0, 0.3)
+    o.pose = start
+    np.testing.assert_allclose(o.poses[-1], start)
+    np.testing.assert_allclose(o.yaw_xy, (1.0, -2.0, 0.3), atol=1e-15)
+    T = _planar(0.2, 0.1, 0.05)
+    o._integrate(T)
+    want, _ = compose(start, T, composition, (1.0, -2.0, 0.3))
+    np.testing.assert_allclose(o.pose, want, atol=1e-12)
+    assert len(o.poses) == 2
+    o.poses = [np.eye(3)]
+    assert len(o.poses) == 1
+    o.yaw_xy = (0.5, 0.5, 0.0)
+    assert o.yaw_xy == (0.5, 0.5, 0.0)
+
+
 def test_lidar_scan_hits_and_noise():
     scene = S.lidar_scene()
     pose = S.lidar_trajectory(1)[0]
