@@ -9,7 +9,8 @@ rank-order sum of 8 partials and the init probe at 8 ranks, which the first 8-GP
 Checked for every case:
   * all ranks end on bit-identical poses, per-iteration poses and losses (the device trace) and statistics;
   * the exchanged statistics equal the one-process shard partials summed in rank order -- bit for bit for the
-    peer exchange (its sum is exactly that), within 1e-12 for the hook (gloo's ring sums in another order);
+    peer exchange (its sum is exactly that), for the hook (gloo's ring sums in another order) within 1e-12 of the
+    partials' summed magnitudes;
   * the registration equals the one-process registration within 1e-9, fixed iterations and converging (1e-8
     if the converging run stops one iteration apart);
   * every rank stops on the same iteration.
@@ -137,8 +138,9 @@ def _check(r, one, world, kind, exact_sum):
         want = _rank_order_sum(parts)
         if exact_sum:
             assert np.array_equal(got, want), np.max(np.abs(got - want))
-        else:
-            scale = np.maximum(np.abs(want), 1e-12 * np.abs(want).max())
+        else:   # a summation-order difference is bounded by the partials' magnitudes, not the sum's (the
+            # gradient entries of a converged pass cancel to ~1e-15 from partials of ~1e-2)
+            scale = np.maximum(np.sum(np.abs(parts), axis=0), 1e-300)
             assert np.max(np.abs(got - want) / scale) < 1e-12
     np.testing.assert_allclose(r[0]["T_fixed"], T1, rtol=0, atol=1e-9)
     # converging: the same stop when the sums' rounding does not move the tolerance test (then 1e-9), else one
