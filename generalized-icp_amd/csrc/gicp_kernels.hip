@@ -119,8 +119,9 @@ struct Stamps {
     unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // realtime (100 MHz) at the end of the certificate + descent phase and at the end of the walk; the walk's
     // kind (0 none, 1 candidate list, 2 list then full walk, 3 full walk); lanes that descended / walked
-    unsigned long long tdesc = 0, twalk = 0;
-    unsigned kind = 0, ndesc = 0, nwalk = 0;
+    unsigned long long tdesc = 0, twalk = 0, ta = 0, tb = 0, te = 0, tf = 0;
+    unsigned kind = 0, ndesc = 0, nwalk = 0, nwalk_jp = 0;
+    float wb0 = 0.f;
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
     __device__ __forceinline__ void count(int k, unsigned v = 1) { cnt[k] += v; }
@@ -130,6 +131,17 @@ struct Stamps {
     __device__ __forceinline__ void count(int, unsigned = 1) {}
 #endif
 };
+
+#ifdef GICP_TIMELINE
+// realtime stamp taken once `a` and `b` are available (their loads complete): the asm's inputs make the
+// compiler wait for them first, and volatile asms keep their order
+template <class A, class B>
+__device__ __forceinline__ unsigned long long tl_after(A a, B b) {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(a), "v"(b) : "memory");
+    return t;
+}
+#endif
 
 // exact-rounding fp64 square distance, summed in axis order without FMA contraction
 // (the order a KD-tree accumulates it in)
@@ -1416,6 +1428,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #ifdef GICP_TIMELINE
     if (A.stamps && l == 0)   // stored at once: no register held across the wave
         A.stamps[((int64_t)blockIdx.x * kCorrWaves + w) * 20 + 16] = __builtin_amdgcn_s_memrealtime();
+    S.ta = tl_after(P.R[0] + st.c[0], cpass0 + hint0 + st.count);   // the prologue's scalar batch is in
 #endif
     if ((A.use_lists || A.cert_j) && blockIdx.x == 0 && threadIdx.x == 0 && !done) {   // this pass's pose into the ring
         double* ring = A.poses + (A.pass % kPoseRing) * 12;
@@ -1511,6 +1524,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 cert = cj >= 0 ? 2.f * cdelta < cgap : cgap - cdelta > A.empty_r;
             }
         }
+#ifdef GICP_TIMELINE
+        S.tb = tl_after(rel.x + cgap, jp);   // the certificates and the point's offset are in
+#endif
         // the point relative to its last match jp, fp32 (error well inside the screen margin): the
         // search cap below and the graph descent start from it
         bool have_jp = false;
@@ -1762,9 +1778,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         ngproved = __popcll(__ballot(gcert));
         nwalked = skip_walk ? 0 : 1;
 #ifdef GICP_TIMELINE
-        S.tdesc = __builtin_amdgcn_s_memrealtime();
+        S.tdesc = tl_after(ngproved, (int)skip_walk);
         S.ndesc = (unsigned)__popcll(__ballot(have_jp));
         S.nwalk = (unsigned)__popcll(__ballot(q.valid && !cert));
+        S.nwalk_jp = (unsigned)__popcll(__ballot(q.valid && !cert && have_jp));
 #endif
         // the widening pays only if the next pass moves the tile by less than kappa / 2: a tile that moved
         // farther than kappa since its last pass (the pose is still converging) walks without it
@@ -1794,6 +1811,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             return fminf(cap, fminf(key_d2(sec), bound_of(key_d2(best))));
         };
         float lb = lane_bound();   // refreshed after every merge
+#ifdef GICP_TIMELINE
+        S.wb0 = __builtin_amdgcn_sqrtf(fmaxf(wave_maxf(lb), 0.f));
+#endif
         // lb inflated by the rounding slack, for the slack-free box tests
         auto inflate = [&](float w) -> float {
             if (w < 0.f) return w;
@@ -1940,7 +1960,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         }
         S.mark(1);
 #ifdef GICP_TIMELINE
-        S.twalk = __builtin_amdgcn_s_memrealtime();
+        S.twalk = tl_after(best, best_tile);
         S.kind = skip_walk ? 0u : use ? 1u : list_rebuilds > 0 ? 2u : 3u;
 #endif
 
@@ -2078,6 +2098,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             if (skip_walk) source_point(s4e);
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
+#ifdef GICP_TIMELINE
+            S.te = tl_after(d2e, ct.x + cs.x);   // the epilogue's gathers are in
+#endif
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = sqrt(d2e);
             // gicp.py:136: reject only if distance > d_c; sqrt(d2) > d_c <=> d2 > dc2_max (host-computed,
             // sqrt is correctly rounded and monotone), so no square root here
@@ -2284,10 +2307,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         o[2] = (unsigned)st.count;
         o[3] = S.tdesc;                                  // certificates + descent done (0: the wave had no tile)
         o[4] = S.twalk;                                  // walk done
-        o[5] = S.kind | (S.ndesc << 8) | (S.nwalk << 16);
-        o[6] = (unsigned)pairs;
-        o[7] = (unsigned)namb_total;
+        o[5] = S.kind | (S.ndesc << 8) | (S.nwalk << 16) | (S.nwalk_jp << 24);
+        o[6] = S.ta;                                     // the prologue's scalar batch in
+        o[7] = S.tb;                                     // certificates in
         for (int c = 0; c < 8; ++c) o[8 + c] = S.cnt[c];
+        o[10] = S.te;                                    // the epilogue's gathers in (0: no accepted lane... none found)
+        o[12] = tl_after(pairs, namb_total);             // statistics GEMM done, before the partials
+        o[14] = __float_as_uint(S.wb0);                  // the walk's starting radius (max over walking lanes)
 #endif
         o[17] = __builtin_amdgcn_s_memrealtime();
         o[18] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID

@@ -23,35 +23,42 @@ sys.path[:0] = [os.path.join(ROOT, "generalized-icp_amd"), ROOT]
 KIND = {0: "none", 1: "list", 2: "list+full", 3: "full"}
 
 
+PH = ("batch", "certs", "descent", "walk", "epi_ld", "gemm", "store")
+
+
 def waves(path):
     a = np.fromfile(path, dtype=np.uint64).reshape(-1, 20).astype(np.int64)
     live = a[:, 17] > 0
     a = a[live]
-    t0 = a[:, 16]
-    base = t0.min()
+    base = a[:, 16].min()
     us = lambda x: (x - base) / 100.0   # noqa: E731  (100 MHz realtime)
     has_tile = a[:, 3] > 0
+    start, end = us(a[:, 16]), us(a[:, 17])
+    ta = np.where(has_tile, us(a[:, 6]), start)
+    tb = np.where(has_tile, us(a[:, 7]), ta)
+    td = np.where(has_tile, us(a[:, 3]), tb)
+    tw = np.where(has_tile, us(a[:, 4]), td)
+    te = np.where(a[:, 10] > 0, us(a[:, 10]), tw)
+    tf = np.where(a[:, 12] > 0, us(a[:, 12]), te)
     w = dict(
-        tile=a[:, 0], start=us(a[:, 16]), end=us(a[:, 17]),
-        desc_end=np.where(has_tile, us(a[:, 3]), us(a[:, 16])),
-        walk_end=np.where(has_tile, us(a[:, 4]), us(a[:, 16])),
-        kind=a[:, 5] & 0xFF, ndesc=(a[:, 5] >> 8) & 0xFF, nwalk=(a[:, 5] >> 16) & 0xFF,
-        pairs=a[:, 6], amb=a[:, 7], visits=a[:, 8], scanned=a[:, 9], list_used=a[:, 11], blk=a[:, 13],
-        fb=a[:, 15], xcc=a[:, 19] & 7)
-    w["t_desc"] = w["desc_end"] - w["start"]
-    w["t_walk"] = w["walk_end"] - w["desc_end"]
-    w["t_epi"] = w["end"] - w["walk_end"]
+        tile=a[:, 0], start=start, end=end,
+        kind=a[:, 5] & 0xFF, ndesc=(a[:, 5] >> 8) & 0xFF, nwalk=(a[:, 5] >> 16) & 0xFF, nwalk_jp=(a[:, 5] >> 24) & 0xFF,
+        visits=a[:, 8], scanned=a[:, 9], list_used=a[:, 11], blk=a[:, 13],
+        wb0=a[:, 14].astype(np.uint32).view(np.float32), fb=a[:, 15], xcc=a[:, 19] & 7)
+    w["ph"] = np.stack([ta - start, tb - ta, td - tb, tw - td, te - tw, tf - te, end - tf])
     return w
 
 
 def describe(w, sel, label):
     k = np.bincount(w["kind"][sel], minlength=4)
-    phase = np.argmax(np.stack([w["t_desc"][sel], w["t_walk"][sel], w["t_epi"][sel]]), axis=0)
-    ph = np.bincount(phase, minlength=3)
-    return (f"  {label:10s} n {sel.sum():5d}  start {np.mean(w['start'][sel]):6.1f}  dur {np.mean((w['end'] - w['start'])[sel]):6.1f}"
-            f"  [desc {np.mean(w['t_desc'][sel]):5.1f} walk {np.mean(w['t_walk'][sel]):5.1f} epi {np.mean(w['t_epi'][sel]):5.1f}]"
-            f"  longest phase d/w/e {ph[0]}/{ph[1]}/{ph[2]}  walk none/list/l+f/full {k[0]}/{k[1]}/{k[2]}/{k[3]}"
-            f"  visits {np.mean(w['visits'][sel]):5.1f}  walkers {np.mean(w['nwalk'][sel]):4.1f}  desc {np.mean(w['ndesc'][sel]):4.1f}")
+    ph = w["ph"][:, sel]
+    top = np.bincount(np.argmax(ph, axis=0), minlength=len(PH))
+    phs = " ".join(f"{n} {np.mean(ph[i]):5.1f}" for i, n in enumerate(PH))
+    tops = "/".join(str(x) for x in top)
+    return (f"  {label:8s} n {sel.sum():5d} start {np.mean(w['start'][sel]):6.1f} dur {np.mean((w['end'] - w['start'])[sel]):5.1f}"
+            f" [{phs}] longest {tops}  walk none/list/l+f/full {k[0]}/{k[1]}/{k[2]}/{k[3]}"
+            f" visits {np.mean(w['visits'][sel]):4.1f} walkers {np.mean(w['nwalk'][sel]):4.1f} (jp {np.mean(w['nwalk_jp'][sel]):4.1f})"
+            f" desc {np.mean(w['ndesc'][sel]):4.1f}")
 
 
 def main():
@@ -84,8 +91,9 @@ def main():
         T, _ = gicp.solve_pose(st, T)
     e.close()
     print(f"n {a.n}  shard 1/{a.shard_sim}  passes {a.passes} (cold, from the identity; gicp_iterate + host solve)")
-    print("per pass: span of the waves (first start -> last end, us) and the waves ending it; phases: desc = prologue +"
-          " certificates + graph descent, walk = list / full walk + fp64 re-resolution start, epi = the rest")
+    print("per pass: span of the waves (first start -> last end, us) and the waves ending it; phases (us): batch = the"
+          " prologue's scalar batch, certs = certificate + point loads, descent = graph descent, walk = list / full walk,"
+          " epi_ld = the epilogue's gathers, gemm = W + statistics GEMM, store = partials + wave end")
     for k in range(a.passes):
         w = waves(os.path.join(tmp, f"st.{first + k}"))
         end = w["end"]
@@ -102,9 +110,10 @@ def main():
             print(describe(w, walkers, "walking"))
         print(describe(w, last1, "last 1%"))
         for i in order[:6]:
-            print(f"    tile {w['tile'][i]:6d} xcc {w['xcc'][i]} start {w['start'][i]:6.1f} desc {w['t_desc'][i]:5.1f}"
-                  f" walk {w['t_walk'][i]:5.1f} ({KIND[int(w['kind'][i])]}, {w['visits'][i]} visits, {w['scanned'][i]} scanned,"
-                  f" {w['nwalk'][i]} walkers) epi {w['t_epi'][i]:5.1f} end {w['end'][i]:6.1f}")
+            phs = " ".join(f"{w['ph'][j, i]:4.1f}" for j in range(len(PH)))
+            print(f"    tile {w['tile'][i]:6d} xcc {w['xcc'][i]} start {w['start'][i]:6.1f} end {w['end'][i]:6.1f} [{phs}]"
+                  f" {KIND[int(w['kind'][i])]}: {w['visits'][i]} visits, {w['scanned'][i]} scanned, {w['nwalk'][i]} walkers"
+                  f" ({w['nwalk_jp'][i]} with a last match), radius {w['wb0'][i]:.3f}, {w['ndesc'][i]} descended")
     for f in os.listdir(tmp):
         os.remove(os.path.join(tmp, f))
     os.rmdir(tmp)
