@@ -255,6 +255,9 @@ struct CorrArgs {
     double* poses;            // [kPoseRing][12] pose of each pass (R row-major, t)
     int32_t pass;             // this pass's id (monotonic per source cloud)
     int32_t use_lists;        // 0: always full walk (no lists)
+    // a wave with 1 .. sparse_max walking lanes searches lane-parallel, one walking lane at a time (the candidate
+    // tiles' rows kSparseGroup tiles per memory round trip) instead of one visit per tile; 0: never
+    int32_t sparse_max;
     float skin;
     // a tile rebuilding its list while the pose still moves uses skin' = min(max(skin, skin_gain x its
     // displacement over the last pass), skin_max): the list then outlasts a step of the same size

@@ -62,6 +62,21 @@ __device__ __forceinline__ float wave_maxf(float v) {
     GICP_WAVE_REDUCE(max, (int)0x80000000, x)
     return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
+__device__ __forceinline__ float readlane_f(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+__device__ __forceinline__ double readlane_d(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// wave minimum of keys < 2^31 (screen keys: non-negative fp32 bits), uniform
+__device__ __forceinline__ unsigned wave_min_key(unsigned v) {
+    int x = (int)v;
+    GICP_WAVE_REDUCE(min, 0x7fffffff, x)
+    return (unsigned)__builtin_amdgcn_readlane(x, 63);
+}
 __device__ __forceinline__ double wave_mind(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
@@ -118,7 +133,7 @@ struct Stamps {
     unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // realtime (100 MHz) at the end of the certificate + descent phase and at the end of the walk; the walk's
-    // kind (0 none, 1 candidate list, 2 list then full walk, 3 full walk); lanes that descended / walked
+    // kind (0 none, 1 candidate list, 2 list then full walk, 3 full walk, 4 sparse search); lanes that descended / walked
     unsigned long long tdesc = 0, twalk = 0, ta = 0, tb = 0, te = 0, tf = 0;
     unsigned kind = 0, ndesc = 0, nwalk = 0, nwalk_jp = 0;
     float wb0 = 0.f;
@@ -1251,6 +1266,10 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
 #ifndef GICP_ROW_SPLIT
 #define GICP_ROW_SPLIT 9
 #endif
+#ifndef GICP_SPARSE_GROUP
+#define GICP_SPARSE_GROUP 4
+#endif
+constexpr int kSparseGroup = GICP_SPARSE_GROUP;   // candidate tiles per round trip of a sparse wave's search
 constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
 
 // In-kernel exchange of a workgroup's NV values with every peer rank (PeerArgs, gicp_internal.h), called by
@@ -1872,6 +1891,159 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
         }
         int ent = 0;   // lane k: list entry k (when the list is used)
+
+        // ---- sparse waves: a lane-parallel search per walking lane ----------------
+        // A wave with a few walking lanes (most of passes 4-19's walking waves have one) walked one visit
+        // per tile, one dependent memory round trip each, its lanes all screening rows for one or two
+        // points.  Here, for one walking lane at a time: its candidate tiles (the source tile's certified
+        // list when that covers the lane, else the super-block / block / tile boxes) are screened
+        // kSparseGroup tiles per round trip with lane r holding row r of each tile (coalesced, no LDS),
+        // every row keyed exactly as scan_tile keys it, the per-lane best and runner-up merged over the
+        // wave after each group (whose new bound prunes the remaining candidates).  Exact: every tile whose
+        // box is within the lane's bound is screened in full and the bound only shrinks; the list is
+        // neither used past its certificate nor rebuilt (it stays valid for its own pose).
+        const uint64_t walkers = skip_walk ? 0ull : __ballot(lb >= 0.f);
+        const bool sparse = walkers != 0ull && __popcll(walkers) <= A.sparse_max;
+        auto sparse_search = [&](int wl) {
+            const Query<D> qp = active_box<D>(q, l == wl);   // the walking lane's point, a conservative box
+            float pw[D];
+#pragma unroll
+            for (int a = 0; a < D; ++a) pw[a] = readlane_f(q.pw[a], wl);
+            const float capw = readlane_f(cap, wl);
+            float wb = readlane_f(lb, wl);
+            unsigned tb = init, ts = init;   // lane r: the best and runner-up key of row r over the tiles screened
+            int tt = -1;                      // ... and the tile of its best
+            unsigned wbest = init, wsec = init;
+            int wtile = -1;
+            const unsigned M = key_mask();
+            auto reduce = [&]() {
+                wbest = wave_min_key(tb);
+                const int win = __ffsll((unsigned long long)__ballot(tb == wbest)) - 1;
+                wsec = wave_min_key(l == win ? ts : tb);
+                wtile = __builtin_amdgcn_readlane(tt, win);
+                wb = fminf(capw, fminf(key_d2(wsec), bound_of(key_d2(wbest))));
+            };
+            // the candidates held by the lanes of `cm` (lane k: tile ct, rows cst .. cst + ccnt, co = the fp32 offset
+            // (float)(ow - c) of the tile's centre c -- the term lane_gap2_ns adds to a lane's pw --, box gap cg)
+            auto screen = [&](uint64_t cm, int ct, int cst, int ccnt, const float* co, float cg) {
+                cm &= __ballot(cg <= wb);
+                while (cm) {
+                    int ks[kSparseGroup];
+                    float rx[kSparseGroup], ry[kSparseGroup], rz[kSparseGroup];
+#pragma unroll
+                    for (int u = 0; u < kSparseGroup; ++u) {   // the group's rows, all requested before any is used
+                        const int k = cm ? __ffsll((unsigned long long)cm) - 1 : -1;
+                        ks[u] = k;
+                        rx[u] = ry[u] = rz[u] = 1e30f;
+                        if (k >= 0) {
+                            cm &= cm - 1;
+                            const int st0 = __builtin_amdgcn_readlane(cst, k), cn = __builtin_amdgcn_readlane(ccnt, k);
+                            if (l < cn) {
+                                const float* rp = reinterpret_cast<const float*>(tg.rel32 + st0 + l);
+                                rx[u] = rp[0];
+                                ry[u] = rp[1];
+                                if (D == 3) rz[u] = rp[2];
+                            }
+                            pairs += cn;
+                            S.count(0);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSparseGroup; ++u) {
+                        const int k = ks[u];
+                        if (k < 0) break;
+                        float pr[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int a = 0; a < D; ++a) pr[a] = pw[a] + readlane_f(co[a], k);
+                        const float dx = pr[0] - rx[u], dy = pr[1] - ry[u];
+                        float d2 = fmaf(dy, dy, dx * dx);
+                        if (D == 3) {
+                            const float dz = pr[2] - rz[u];
+                            d2 = fmaf(dz, dz, d2);
+                        }
+                        const unsigned key = (__float_as_uint(d2) & M) | (unsigned)l;
+                        ts = umed3(tb, ts, key);
+                        if (key < tb) tt = __builtin_amdgcn_readlane(ct, k);
+                        tb = min(tb, key);
+                    }
+                    reduce();
+                    cm &= __ballot(cg <= wb);
+                }
+            };
+            bool covered = false;
+            if (use) {   // the list's entries near this lane, then whether the list covers its final bound
+                int lt = 0, lst = 0, lcn = 0;
+                float lc[3] = {0.f, 0.f, 0.f};
+                float lg = 3e38f;
+                if (l < nl) {
+                    lt = A.list[(int64_t)T * kListMax + l];
+                    const TileBox tbx = tg.boxes[lt];
+                    lg = gap2_box<D>(qp, tbx.c, tbx.h);
+#pragma unroll
+                    for (int a = 0; a < D; ++a) lc[a] = (float)(q.ow[a] - tbx.c[a]);
+                    lst = tbx.start;
+                    lcn = tbx.count;
+                }
+                screen(__ballot(l < nl), lt, lst, lcn, lc, lg);
+                covered = __builtin_amdgcn_sqrtf(fmaxf(wb, 0.f)) * 1.0001f + delta <= rc;
+                if (!covered) {   // start over with the bound the list gave (every tile within it is rescreened)
+                    tb = ts = init;
+                    tt = -1;
+                }
+            }
+            if (!covered) {   // super-blocks -> blocks -> tiles against the lane's box, as walk_c
+                const int nsuper = (tg.nblocks + kWave - 1) / kWave;
+                for (int s0 = 0; s0 < nsuper; s0 += kWave) {
+                    float sg = 3e38f;
+                    if (s0 + l < nsuper) sg = gap2_box<D>(qp, tg.blocks[tg.nblocks + s0 + l].c, tg.blocks[tg.nblocks + s0 + l].h);
+                    uint64_t sm = __ballot(sg <= wb);
+                    while (sm) {
+                        const int sl = __ffsll((unsigned long long)sm) - 1;
+                        sm &= sm - 1;
+                        if (!(readlane_f(sg, sl) <= wb)) continue;
+                        const int b0 = (s0 + sl) * kWave, b = b0 + l;
+                        float bg = 3e38f;
+                        if (b < tg.nblocks) bg = gap2_box<D>(qp, tg.blocks[b].c, tg.blocks[b].h);
+                        uint64_t bm = __ballot(bg <= wb);
+                        while (bm) {
+                            const int bl = __ffsll((unsigned long long)bm) - 1;
+                            bm &= bm - 1;
+                            if (!(readlane_f(bg, bl) <= wb)) continue;
+                            const int first = (b0 + bl) * kBlockTiles, nt = min(kBlockTiles, tg.ntiles - first);
+                            int ht = first + l, hst = 0, hcn = 0;
+                            float hc[3] = {0.f, 0.f, 0.f};
+                            float hg = 3e38f;
+                            if (l < nt) {
+                                const TileBox tbx = tg.boxes[ht];
+                                hg = gap2_box<D>(qp, tbx.c, tbx.h);
+#pragma unroll
+                                for (int a = 0; a < D; ++a) hc[a] = (float)(q.ow[a] - tbx.c[a]);
+                                hst = tbx.start;
+                                hcn = tbx.count;
+                            }
+                            screen(__ballot(l < nt), ht, hst, hcn, hc, hg);
+                        }
+                    }
+                }
+            }
+            if (l == wl) {
+                best = wbest;
+                sec = wsec;
+                best_tile = wtile;
+            }
+        };
+        if (sparse) {
+            uint64_t wm = walkers;
+            while (wm) {
+                const int wl = __ffsll((unsigned long long)wm) - 1;
+                wm &= wm - 1;
+                sparse_search(wl);
+            }
+            lb = lane_bound();
+            lbx = inflate(lb);
+        }
+        const bool use_sparse = sparse;   // (the walk's kind, diagnostics)
+        if (sparse) use = false;
         if (use) {
             S.count(3);
             S.count(4, nl);
@@ -1921,7 +2093,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 ++list_rebuilds;
             }
         }
-        if (!use && !skip_walk) {
+        if (!use && !skip_walk && !sparse) {
             float skin = A.skin;   // adaptive: a moving tile's list covers a step like its last one
             if (lists && A.skin_gain > 0.f) {
                 const float dl = disp_since(A.pass - 1);
@@ -1961,7 +2133,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         S.mark(1);
 #ifdef GICP_TIMELINE
         S.twalk = tl_after(best, best_tile);
-        S.kind = skip_walk ? 0u : use ? 1u : list_rebuilds > 0 ? 2u : 3u;
+        S.kind = skip_walk ? 0u : use_sparse ? 4u : use ? 1u : list_rebuilds > 0 ? 2u : 3u;
 #endif
 
         // the fp64 source point is needed only from here on (kept out of the walk's registers).  A wave

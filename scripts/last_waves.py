@@ -20,7 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "generalized-icp_amd"), ROOT]
 
-KIND = {0: "none", 1: "list", 2: "list+full", 3: "full"}
+KIND = {0: "none", 1: "list", 2: "list+full", 3: "full", 4: "sparse"}
 
 
 PH = ("batch", "certs", "descent", "walk", "epi_ld", "gemm", "store")
@@ -50,13 +50,13 @@ def waves(path):
 
 
 def describe(w, sel, label):
-    k = np.bincount(w["kind"][sel], minlength=4)
+    k = np.bincount(w["kind"][sel], minlength=5)
     ph = w["ph"][:, sel]
     top = np.bincount(np.argmax(ph, axis=0), minlength=len(PH))
     phs = " ".join(f"{n} {np.mean(ph[i]):5.1f}" for i, n in enumerate(PH))
     tops = "/".join(str(x) for x in top)
     return (f"  {label:8s} n {sel.sum():5d} start {np.mean(w['start'][sel]):6.1f} dur {np.mean((w['end'] - w['start'])[sel]):5.1f}"
-            f" [{phs}] longest {tops}  walk none/list/l+f/full {k[0]}/{k[1]}/{k[2]}/{k[3]}"
+            f" [{phs}] longest {tops}  walk none/list/l+f/full/sparse {k[0]}/{k[1]}/{k[2]}/{k[3]}/{k[4]}"
             f" visits {np.mean(w['visits'][sel]):4.1f} walkers {np.mean(w['nwalk'][sel]):4.1f} (jp {np.mean(w['nwalk_jp'][sel]):4.1f})"
             f" desc {np.mean(w['ndesc'][sel]):4.1f}")
 
@@ -105,6 +105,12 @@ def main():
         walkers = w["nwalk"] > 0
         print(f"pass {k:2d}: span {span:6.1f} us  waves {len(end)}  walking waves {walkers.sum()}"
               f" (<= 8 walkers: {(walkers & (w['nwalk'] <= 8)).sum()})  p50 end {np.median(end):6.1f}  p99 end {np.percentile(end, 99):6.1f}")
+        one = (w["ndesc"] == 1) & (w["nwalk"] == 0)   # waves whose only search was one lane's graph descent
+        many = (w["ndesc"] >= 16) & (w["nwalk"] == 0)
+        if one.any() or many.any():
+            print(f"  descent phase: waves with 1 descending lane (no walk) n {one.sum()} mean"
+                  f" {np.mean(w['ph'][2][one]) if one.any() else float('nan'):5.2f} us; >= 16 lanes n {many.sum()} mean"
+                  f" {np.mean(w['ph'][2][many]) if many.any() else float('nan'):5.2f} us")
         print(describe(w, np.ones(len(end), bool), "all"))
         if walkers.any():
             print(describe(w, walkers, "walking"))
