@@ -4,12 +4,14 @@
 // it right after the statistics reduction (one launch and one kernel boundary fewer per
 // iteration).
 //
-// solve_pose_t (gicp_solver.h) restated for one wave inside k_corr's register budget (80 VGPRs at 6 waves
-// per SIMD, no scratch frame).  The set-up (K = Htt^-1 Htr, the reduced Hessian H', g', c0') is lane-parallel
-// through LDS; the Newton iterations hold row i of H' in lane i's registers and every uniform value (R,
-// dr = R - R_k, the gradient, the M x M system) in scalar registers, and meet through cross-lane reads (DPP
-// row sums, readlane) rather than LDS barriers; the M x M system runs redundantly in every lane (uniform
-// control flow).  Same iterates as the serial solver up to summation order.
+// Register-lean: solve_pose_t (gicp_solver.h) restated so that only lane-distributed values live in
+// registers across its phases.  The reduced NR x NR Hessian H' is held one row per lane (lane i < NR) in
+// LDS, the uniform rotation iterates (R, the trial Rn, R_k), K = Htt^-1 Htr and the result pose in LDS too;
+// each phase reads what it needs and writes what the next one needs, so the solve fits k_corr's register
+// budget (80 VGPRs at 6 waves per SIMD) without a scratch frame.  The matrix-vector products (H' dr,
+// H' vec(G_l R), the loss) are lane-parallel and meet through LDS; the M x M Newton system and the rotation
+// update run redundantly in every lane (uniform control flow).  Same iterates as the serial solver up to
+// summation order.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -33,67 +35,18 @@ __device__ __forceinline__ void solve_sync() {
     asm volatile("" ::: "memory");
 }
 
-// Cross-lane helpers of the Newton iterations (uniform results are scalar registers)
-__device__ __forceinline__ double readlane_dbl(double v, int k) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double wave_uniform(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_dbl(double x) {   // lanes outside the row read 0 (old value)
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// sum of lanes 0..15 (row_shr 1, 2, 4, 8: lane 15 ends with the row's sum), uniform
-__device__ __forceinline__ double row_sum16(double x) {
-    x += dpp_dbl<0x111>(x);
-    x += dpp_dbl<0x112>(x);
-    x += dpp_dbl<0x114>(x);
-    x += dpp_dbl<0x118>(x);
-    return readlane_dbl(x, 15);
-}
-__device__ __forceinline__ double sel3(int b, double x0, double x1, double x2) { return b == 0 ? x0 : b == 1 ? x1 : x2; }
-__device__ __forceinline__ double sel4(int i, double x0, double x1, double x2, double x3) {
-    return i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
-}
-template <int N>
-__device__ __forceinline__ double sel_arr(int i, const double (&a)[N]) {
-    double v = a[0];
-#pragma unroll
-    for (int j = 1; j < N; ++j) v = i == j ? a[j] : v;
-    return v;
-}
-// entry (a, b) of exp([w]) R from column b of R (c0, c1, c2 = R_0b, R_1b, R_2b): exp_mul_entry's formula with
-// the row a a per-lane value
-__device__ __forceinline__ double exp_mul_entry_col(const double* w, double s1, double s2, double c, double c0,
-                                                    double c1, double c2, int a) {
-    const double wa = a == 0 ? w[0] : a == 1 ? w[1] : w[2];
-    const double x0 = a == 0 ? 0.0 : a == 1 ? w[2] : -w[1];
-    const double x1 = a == 0 ? -w[2] : a == 1 ? 0.0 : w[0];
-    const double x2 = a == 0 ? w[1] : a == 1 ? -w[0] : 0.0;
-    const double e0 = (a == 0 ? c : 0.0) + s2 * wa * w[0] + s1 * x0;
-    const double e1 = (a == 1 ? c : 0.0) + s2 * wa * w[1] + s1 * x1;
-    const double e2 = (a == 2 ? c : 0.0) + s2 * wa * w[2] + s1 * x2;
-    return e0 * c0 + e1 * c1 + e2 * c2;
-}
-
 // LDS of the one-wave solve
 template <int D>
 struct SolveLds {
     static constexpr int NR = D * D, M = D == 2 ? 1 : 3, N1 = D + 1;
+    double hrow[NR][NR];        // row i of H' (written and read by lane i)
     double kc[D][NR];           // K = Htt^-1 Htr, column i from lane i
     double kt[D];               // Htt^-1 gt
-    double hrow[NR][NR];        // row i of H' (written and read by lane i)
-    double R[NR], Rk[NR];       // the solved and the starting rotation (row-major)
+    double R[NR], Rn[NR], Rk[NR];   // current, trial and starting rotation (row-major)
+    double dr[NR];              // Rn - Rk
+    double u[NR], hd[M][NR];    // u = H' dr - g' and H' vec(G_l R), lane-distributed
+    double pq[NR + M * (M + 1) / 2];   // P = R U^T, then vec(G_k R).(H' vec(G_l R)) for l >= k
+    double f[2][NR];            // loss partials, double-buffered: one barrier per evaluation
     double T[N1 * N1];          // the result pose
 };
 
@@ -146,7 +99,7 @@ __device__ __forceinline__ bool solve_pose_wave(const double* st, const double* 
             for (int a = 0; a < D; ++a) sl.kt[a] = kt[a];
     }
     solve_sync();
-    // row i of H' (LDS, lane i's) and g'_i; c0' (uniform)
+    // row i of H' and g'_i; c0' (uniform)
     double gpi, c0p;
     {
         const int ia = i / D, ii = i % D;
@@ -168,95 +121,99 @@ __device__ __forceinline__ bool solve_pose_wave(const double* st, const double* 
         for (int a = 0; a < D; ++a) c0p -= gt[a] * sl.kt[a];
     }
 
-    // The Newton iterations keep every uniform value in scalar registers and exchange lane values through
-    // cross-lane reads instead of LDS round trips (round 6: the LDS form's five barrier phases per step were
-    // most of its ~1.5 us): lane i < NR holds row i of H' in registers; R and dr = R - R_k are uniform; the
-    // gradient and the reduced Hessian are sums over the NR lanes (DPP row sums); the trial rotation's
-    // entries are computed one per lane and read back by every lane; the loss at the trial rotation is
-    // summed in lane order, the serial solver's order.
-    const double gpl = lane < NR ? gpi : 0.0;
-    const double* const Hr = sl.hrow[lane < NR ? lane : 0];   // lanes >= NR read row 0 and weigh it by 0
-    double R[NR];
+    // loss at Rn (phi of the serial solver) and, on lane i, u_i = (H' dr - g')_i
+    int fbuf = 0;
+    auto eval = [&](double& ui) -> double {
+        double hi = 0.0;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) R[j] = wave_uniform(sl.Rk[j]);
-    double hdr = 0.0;   // (H' dr)_i at the current R (dr = R - R_k = 0 at the start)
-    const double Rkl = lane < NR ? sl.Rk[lane] : 0.0;   // this lane's entry of R_k
-    const int la = (lane < NR ? lane : 0) / D, lb = (lane < NR ? lane : 0) % D;
-    // column b of R for this lane's entry i = (a, b): cl[c] = R_cb (3-D); 2-D cl = (R_0b, R_1b)
-    double cl[D];
-    auto load_col = [&]() {
-        if constexpr (D == 2) {
-            cl[0] = (lb == 0) ? R[0] : R[1];
-            cl[1] = (lb == 0) ? R[2] : R[3];
-        } else {
-            cl[0] = sel3(lb, R[0], R[1], R[2]);
-            cl[1] = sel3(lb, R[3], R[4], R[5]);
-            cl[2] = sel3(lb, R[6], R[7], R[8]);
-        }
-    };
-    // vec(G_k R)_i (3-D: rows of G_k R are +-rows of R or 0; 2-D: G R = (-R[2], -R[3], R[0], R[1]))
-    auto gen_entry = [&](int k) -> double {
-        if constexpr (D == 2) {
-            return la == 0 ? -cl[1] : cl[0];
-        } else {
-            if (k == 0) return la == 0 ? 0.0 : la == 1 ? -cl[2] : cl[1];
-            if (k == 1) return la == 0 ? cl[2] : la == 1 ? 0.0 : -cl[0];
-            return la == 0 ? -cl[1] : la == 1 ? cl[0] : 0.0;
-        }
-    };
-    // vec(1/2 (G_k G_l + G_l G_k) R)_i: 3-D 1/2 ([a == l] R_kb + [a == k] R_lb) - delta_kl R_ab; 2-D -R_i
-    auto sym2_entry = [&](int k, int l) -> double {
-        if constexpr (D == 2) {
-            return -(la == 0 ? cl[0] : cl[1]);
-        } else {
-            const double rab = la == 0 ? cl[0] : la == 1 ? cl[1] : cl[2];
-            return 0.5 * ((la == l ? cl[k] : 0.0) + (la == k ? cl[l] : 0.0)) - (k == l ? rab : 0.0);
-        }
-    };
-    // the loss at rotation Rn (one entry per lane: rn = Rn_i) -- phi of the serial solver: f = c0' + sum_i
-    // (dr_i (H' dr)_i - 2 g'_i dr_i), summed in lane order; leaves (H' dr_n)_i in hi
-    auto eval = [&](double rn, double& hi) -> double {
-        const double dl = lane < NR ? rn - Rkl : 0.0;
-        hi = 0.0;
-#pragma unroll
-        for (int j = 0; j < NR; ++j) hi += Hr[j] * readlane_dbl(dl, j);
-        const double term = dl * hi - 2.0 * gpl * dl;
+        for (int j = 0; j < NR; ++j) hi += sl.hrow[i][j] * sl.dr[j];
+        const double dri = sl.dr[i];
+        ui = hi - gpi;
+        // alternate buffers: a buffer is rewritten two evaluations later, and every path between
+        // passes a barrier after its reads (this eval's or the next iteration's), so no second one here
+        double* const fb = sl.f[fbuf];
+        fbuf ^= 1;
+        if (lane < NR) fb[lane] = dri * hi - 2.0 * gpi * dri;
+        solve_sync();
         double f = c0p;
 #pragma unroll
-        for (int j = 0; j < NR; ++j) f += readlane_dbl(term, j);
+        for (int j = 0; j < NR; ++j) f += fb[j];
         return f;
     };
 
-    double f = c0p;   // at R = R_k: dr = 0, the loss is c0' exactly
+    // at R = R_k: dr = 0, so u_i = -g'_i and the loss is c0' exactly (what eval(R_k) would return)
+    double ui = -gpi;
+    double f = c0p;
     double lam = 0.0;
     GICP_SOLVE_STAMP(3);
     for (int it = 0; it < 100; ++it) {
         GICP_SOLVE_STAMP(4 + min(it, 3));
+        if (lane < NR) {
+            sl.u[lane] = ui;
+            double Rr[NR], Hr[NR];
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                Rr[k] = sl.R[k];
+                Hr[k] = sl.hrow[lane][k];
+            }
+#pragma unroll
+            for (int l = 0; l < M; ++l) sl.hd[l][lane] = gdot<D>(l, Rr, Hr);   // (H' vec(G_l R))_i
+        }
+        solve_sync();
+        GICP_SOLVE_STAMP(8);
+        // grad_k = 2 u.vec(G_k R) and the second-order term u.vec(1/2 (G_k G_l + G_l G_k) R) of the
+        // serial solver, through P = R U^T (U = u as a D x D matrix): u.vec(X R) = tr(X P),
+        // G_k G_l = e_l e_k^T - delta_kl I in 3-D and G^2 = -I in 2-D.  The entries of P and the M(M+1)/2
+        // products vec(G_k R).(H' vec(G_l R)) come one per lane.
         constexpr int NH = M * (M + 1) / 2;
+        if (lane < NR) {
+            const int a = lane / D, b = lane % D;
+            double p = 0.0;
+#pragma unroll
+            for (int c = 0; c < D; ++c) p += sl.R[a * D + c] * sl.u[b * D + c];
+            sl.pq[lane] = p;
+        } else if (lane < NR + NH) {
+            const int q = lane - NR;   // (k, l), l >= k, in row order
+            const int k = M == 1 ? 0 : (q < 3 ? 0 : q < 5 ? 1 : 2);
+            const int l = M == 1 ? 0 : (q < 3 ? q : q < 5 ? q - 2 : 2);
+            double Rr[NR], hv[NR];
+#pragma unroll
+            for (int c = 0; c < NR; ++c) {
+                Rr[c] = sl.R[c];
+                hv[c] = sl.hd[l][c];
+            }
+            sl.pq[lane] = gdot<D>(k, Rr, hv);
+        }
+        solve_sync();
         double grad[M], Hs[M][M];
         {
-            const double u = hdr - gpl;   // (H' dr - g')_i
-            load_col();
-            double gk[M], hd[M];
+            double P[D][D];
 #pragma unroll
-            for (int k = 0; k < M; ++k) {
-                gk[k] = lane < NR ? gen_entry(k) : 0.0;
-                hd[k] = gdot<D>(k, R, Hr);   // (H' vec(G_k R))_i
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int b = 0; b < D; ++b) P[a][b] = sl.pq[a * D + b];
+            if constexpr (D == 2) {
+                grad[0] = 2.0 * (P[0][1] - P[1][0]);
+            } else {
+                grad[0] = 2.0 * (P[1][2] - P[2][1]);
+                grad[1] = 2.0 * (P[2][0] - P[0][2]);
+                grad[2] = 2.0 * (P[0][1] - P[1][0]);
             }
-            GICP_SOLVE_STAMP(8);
+            double trP = 0.0;
 #pragma unroll
-            for (int k = 0; k < M; ++k) grad[k] = 2.0 * row_sum16(u * gk[k]);
-            int q = 0;
+            for (int a = 0; a < D; ++a) trP += P[a][a];
+            int q = NR;
 #pragma unroll
             for (int k = 0; k < M; ++k)
 #pragma unroll
-                for (int l = k; l < M; ++l, ++q) {
-                    const double c = lane < NR ? gk[k] * hd[l] + u * sym2_entry(k, l) : 0.0;
-                    Hs[k][l] = Hs[l][k] = 2.0 * row_sum16(c);
+                for (int l = k; l < M; ++l) {
+                    const double t2 = D == 2 ? -trP : 0.5 * (P[k][l] + P[l][k]) - (k == l ? trP : 0.0);
+                    Hs[k][l] = Hs[l][k] = 2.0 * sl.pq[q++] + 2.0 * t2;
                 }
-            (void)NH;
         }
         GICP_SOLVE_STAMP(9);
+        // (no barrier here: u / hd are rewritten only after the eval below, whose barriers order these
+        // reads; every path to the next iteration runs it)
         double gmax = 0.0, hscale = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -286,19 +243,15 @@ __device__ __forceinline__ bool solve_pose_wave(const double* st, const double* 
             }
             GICP_SOLVE_STAMP(10);
             if (ok) {
-                double rn;   // this lane's entry of exp([w]) R
-                if constexpr (D == 2) {
-                    double c, s;
-                    sincos_lean(w[0], s, c);
-                    rn = la == 0 ? c * cl[0] - s * cl[1] : s * cl[0] + c * cl[1];
-                } else {
-                    double s1, s2, c;
-                    exp_coeffs(w, s1, s2, c);
-                    rn = exp_mul_entry_col(w, s1, s2, c, cl[0], cl[1], cl[2], la);
+                if (lane < NR) {   // one entry per lane
+                    const double rn = rot_update_entry<D>(w, sl.R, lane);
+                    sl.Rn[lane] = rn;
+                    sl.dr[lane] = rn - sl.Rk[lane];
                 }
+                solve_sync();
                 GICP_SOLVE_STAMP(11);
-                double hn;
-                const double fn = eval(rn, hn);
+                double un;
+                const double fn = eval(un);
                 wmax = 0.0;
 #pragma unroll
                 for (int k = 0; k < M; ++k) wmax = fmax(wmax, fabs(w[k]));
@@ -310,10 +263,9 @@ __device__ __forceinline__ bool solve_pose_wave(const double* st, const double* 
                 }
                 if (fn <= f || wmax < kc(1e-15)) {
                     if (fn <= f) {
-#pragma unroll
-                        for (int j = 0; j < NR; ++j) R[j] = readlane_dbl(rn, j);
-                        hdr = hn;
+                        if (lane < NR) sl.R[lane] = sl.Rn[lane];
                         f = fn;
+                        ui = un;
                     }
                     stepped = true;
                     quad = fn <= f && lam == 0.0 && wmax < kc(kQuadStop);   // (f = fn when accepted)
@@ -325,8 +277,8 @@ __device__ __forceinline__ bool solve_pose_wave(const double* st, const double* 
             lam = lam == 0.0 ? kc(1e-9) : lam * kc(10.0);
         }
         if (!stepped || flat || quad || wmax < kc(1e-15)) break;
+        solve_sync();   // the accepted R before the next iteration's reads
     }
-    if (lane < NR) sl.R[lane] = sel_arr<NR>(lane, R);
     solve_sync();
     GICP_SOLVE_STAMP(12);
     // t from the eliminated block
