@@ -1905,10 +1905,18 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         const uint64_t walkers = skip_walk ? 0ull : __ballot(lb >= 0.f);
         const bool sparse = walkers != 0ull && __popcll(walkers) <= A.sparse_max;
         auto sparse_search = [&](int wl) {
-            const Query<D> qp = active_box<D>(q, l == wl);   // the walking lane's point, a conservative box
             float pw[D];
 #pragma unroll
             for (int a = 0; a < D; ++a) pw[a] = readlane_f(q.pw[a], wl);
+            // the walking lane's point as a box: what active_box<D>(q, l == wl) gives for one lane (centre ow + pw,
+            // half-extent its padding for pw's rounding, 4.8e-7 (|lo| + |hi| + 2 ew)), without its wave reductions
+            Query<D> qp = q;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                const float B = 2.f * q.ew[a] + 1e-30f;
+                qp.ow[a] = q.ow[a] + (double)pw[a];
+                qp.ew[a] = 4.8e-7f * (2.f * fabsf(pw[a]) + B) + 1e-30f;
+            }
             const float capw = readlane_f(cap, wl);
             float wb = readlane_f(lb, wl);
             unsigned tb = init, ts = init;   // lane r: the best and runner-up key of row r over the tiles screened
@@ -1986,6 +1994,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 }
                 screen(__ballot(l < nl), lt, lst, lcn, lc, lg);
                 covered = __builtin_amdgcn_sqrtf(fmaxf(wb, 0.f)) * 1.0001f + delta <= rc;
+                if (covered) S.count(3);
                 if (!covered) {   // start over with the bound the list gave (every tile within it is rescreened)
                     tb = ts = init;
                     tt = -1;
@@ -2001,6 +2010,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         const int sl = __ffsll((unsigned long long)sm) - 1;
                         sm &= sm - 1;
                         if (!(readlane_f(sg, sl) <= wb)) continue;
+                        S.count(5);
                         const int b0 = (s0 + sl) * kWave, b = b0 + l;
                         float bg = 3e38f;
                         if (b < tg.nblocks) bg = gap2_box<D>(qp, tg.blocks[b].c, tg.blocks[b].h);
@@ -2009,6 +2019,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                             const int bl = __ffsll((unsigned long long)bm) - 1;
                             bm &= bm - 1;
                             if (!(readlane_f(bg, bl) <= wb)) continue;
+                            S.count(6);
                             const int first = (b0 + bl) * kBlockTiles, nt = min(kBlockTiles, tg.ntiles - first);
                             int ht = first + l, hst = 0, hcn = 0;
                             float hc[3] = {0.f, 0.f, 0.f};

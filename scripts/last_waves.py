@@ -114,6 +114,11 @@ def main():
         print(describe(w, np.ones(len(end), bool), "all"))
         if walkers.any():
             print(describe(w, walkers, "walking"))
+        sp = w["kind"] == 4
+        if sp.any():
+            print(f"  sparse waves n {sp.sum()}: walk {np.mean(w['ph'][3][sp]):5.2f} us, walkers covered by the list"
+                  f" {np.mean(w['list_used'][sp]):4.2f} / wave, candidate super-blocks {np.mean(w['blk'][sp]):4.2f} / wave,"
+                  f" tiles screened {np.mean(w['visits'][sp]):5.1f} / wave")
         print(describe(w, last1, "last 1%"))
         for i in order[:6]:
             phs = " ".join(f"{w['ph'][j, i]:4.1f}" for j in range(len(PH)))
