@@ -1585,14 +1585,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     cpw = pair_code(__uint_as_float(cpw & 0xffff0000u), cj - cj2);
                     cj = cj2;
                 }
-                // the single certificate now: the runner-up is the pair's other point (exact gap) or one of the rest
-                // (>= G3 - 2 delta farther), written as a gap relative to cert_pass (the restated certificate subtracts
-                // 2 delta again; the (1 - 1e-6) factors cover the fp32 round trip)
+                // their exact gap now, as a gap relative to cert_pass (the restated certificate subtracts 2 delta
+                // again; the (1 - 1e-6) factors cover the fp32 round trip)
                 const double g = (sqrt(sw ? da : db) - sqrt(sw ? db : da)) * (1.0 - 1e-6) - 1e-12;
-                const float g12 = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
-                const float gs = fminf(g12, (__uint_as_float(cpw & 0xffff0000u) - 2.f * cdelta) * (1.0f - 1e-6f));
-                // (two fp32 roundings of the round trip, each <= 2^-23 (gs + 2 delta), taken off first)
-                cgap = fmaxf(gs - 2.5e-7f * (gs + 2.f * cdelta), 0.f) + 2.f * cdelta;
+                cgap = (g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f) + 2.f * cdelta;
                 cert = true;
             }
         }
