@@ -329,10 +329,7 @@ struct gicp_ctx {
     int32_t* d_cert_j = nullptr;
     float* d_cert_gap = nullptr;
     int32_t* d_cert_pass = nullptr;
-    size_t cap_cj = 0, cap_cg = 0, cap_cp = 0, cap_cpr = 0;
-    uint32_t* d_cert_pair = nullptr;  // CorrArgs::cert_pair
-    bool use_pairs = true;            // GICP_NO_PAIRS=1: no pair certificates
-    double pair_gap_frac = 0.004;     // CorrArgs::pair_gap as a fraction of d_c (GICP_PAIR_GAP)
+    size_t cap_cj = 0, cap_cg = 0, cap_cp = 0;
     bool use_certs = true;            // GICP_NO_CERTS=1: every pass walks every lane
     bool use_graph = true;            // GICP_NO_GRAPH=1: no target neighbour graph, no graph descent
     bool fuse_solve = true;           // GICP_FUSE_SOLVE=0: the solve as its own k_solve launch even with no exchange
@@ -832,7 +829,6 @@ void set_shard(gicp_ctx* c, int shard, int nshards) {
     if (!c->d_poses) dalloc(c->d_poses, (size_t)kPoseRing * 12);
     dreserve(c->d_cert_j, c->cap_cj, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_gap, c->cap_cg, (size_t)std::max<int64_t>(1, c->src.n));
-    dreserve(c->d_cert_pair, c->cap_cpr, (size_t)std::max<int64_t>(1, c->src.n));
     dreserve(c->d_cert_pass, c->cap_cp, nt);
     reset_tile_state(c);
 }
@@ -893,8 +889,6 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     if (c->use_certs) {
         a.cert_j = c->d_cert_j;
         a.cert_gap = c->d_cert_gap;
-        if (c->use_pairs) a.cert_pair = c->d_cert_pair;   // (read only where cert_j >= 0, written with it)
-        a.pair_gap = (float)(c->pair_gap_frac * dc);
     }
     a.cert_pass = c->d_cert_pass;   // always valid: k_corr reads it (and hint) unconditionally, with the tile metadata
     a.hint = c->d_hint;
@@ -1169,8 +1163,6 @@ int gicp_create(gicp_ctx** out, int device) {
     if (const char* e = std::getenv("GICP_SKIN")) c->skin_frac = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_SKIN_GAIN")) c->skin_gain = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_CERTS")) c->use_certs = !(e[0] == '1');
-    if (const char* e = std::getenv("GICP_NO_PAIRS")) c->use_pairs = !(e[0] == '1');
-    if (const char* e = std::getenv("GICP_PAIR_GAP")) c->pair_gap_frac = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_NO_GRAPH")) c->use_graph = !(e[0] == '1');
     if (const char* e = std::getenv("GICP_FUSE_SOLVE")) c->fuse_solve = !(e[0] == '0');
     if (const char* e = std::getenv("GICP_UNIT_MAP")) c->unit_map = std::max(0, std::atoi(e));
@@ -1229,7 +1221,6 @@ void gicp_destroy(gicp_ctx* c) {
     dfree(c->d_top_tgt);
     dfree(c->d_cert_j);
     dfree(c->d_cert_gap);
-    dfree(c->d_cert_pair);
     dfree(c->d_cert_pass);
     dfree(c->d_top_v);
     dfree(c->d_top_i);

@@ -265,12 +265,6 @@ struct CorrArgs {
     // per-source-point nearest-neighbour certificates, sorted source order; null: off
     int32_t* cert_j;          // [src.n] sorted target index of the certified nearest, -1: none within R
     float* cert_gap;          // [src.n] runner-up gap (found) or empty radius R (none), relative to cert_pass
-    // [src.n] pair certificate (null: off), 0 = none, else (bits of G3 truncated to the upper 16) |
-    // (uint16)(j2 - cert_j): relative to cert_pass every target but cert_j and j2 is >= G3 farther than cert_j, so
-    // while 2 delta < G3 the nearest is one of the two (resolved exactly); produced by a proof whose runner-up
-    // gap is below pair_gap (m)
-    uint32_t* cert_pair;
-    float pair_gap;
     int32_t* cert_pass;       // [src.ntiles] pass the tile's certificates refer to (-1: none)
     float kappa;              // runner-up gap the walk resolves (m); 0 without certificates
     float empty_r;            // d_c (fp32, rounded up): a lane with no target within R - delta > empty_r stays rejected

@@ -158,14 +158,6 @@ __device__ __forceinline__ unsigned long long tl_after(A a, B b) {
 }
 #endif
 
-// Pair certificate word (CorrArgs::cert_pair): G3 truncated to its upper 16 bits (a smaller gap: still sound) and
-// the runner-up as a 16-bit offset from the certified index; 0 (none) when either does not fit
-__device__ __forceinline__ uint32_t pair_code(float g3, int delta) {
-    if (!(g3 > 0.f) || delta == 0 || delta < -32768 || delta > 32767) return 0u;
-    const uint32_t hi = __float_as_uint(g3) & 0xffff0000u;
-    return hi ? (hi | (uint32_t)(delta & 0xffff)) : 0u;
-}
-
 // exact-rounding fp64 square distance, summed in axis order without FMA contraction
 // (the order a KD-tree accumulates it in)
 template <int D>
@@ -1541,55 +1533,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         int cj = -1;
         float cgap = 0.f, cdelta = -1.f;
         int jp = -1;   // the point's last match (loaded unconditionally: in flight with cert_pass)
-        // pair certificate word of the lane (0: none): for a certified lane relative to cert_pass
-        // (the nearest is cj or cj + delta while 2 delta < G3), for one the descent proves, relative to this pass
-        uint32_t cpw = 0u;
-        bool pairl = false;   // the lane's single certificate failed and its pair resolves it
         if (A.cert_j) {
             jp = A.cert_j[i];
             const float g0 = A.cert_gap[i];
-            const uint32_t cp0 = A.cert_pair ? A.cert_pair[i] : 0u;
             cdelta = disp_since(cpass0);
             if (cdelta >= 0.f && q.valid) {
                 cj = jp;
                 cgap = g0;
                 cert = cj >= 0 ? 2.f * cdelta < cgap : cgap - cdelta > A.empty_r;
-                if (cj >= 0) {
-                    cpw = cp0;
-                    const int cj2 = cj + (int)(short)(cp0 & 0xffffu);
-                    pairl = cp0 != 0u && !cert && 2.f * cdelta < __uint_as_float(cp0 & 0xffff0000u) && cj2 >= 0 &&
-                            cj2 < tg.n;
-                }
-            }
-        }
-        // pair lanes: the two candidates' exact distances (and the KD-tree's tie rule) decide, in one round trip
-        if (A.cert_pair && wave_any(pairl)) {
-            if (pairl) {
-                const int cj2 = cj + (int)(short)(cpw & 0xffffu);
-                const double4 s4 = reinterpret_cast<const double4*>(sc.xyz64)[i];
-                const double4 a4 = reinterpret_cast<const double4*>(tg.xyz64)[cj];
-                const double4 b4 = reinterpret_cast<const double4*>(tg.xyz64)[cj2];
-                const int oa = tg.perm[cj], ob = tg.perm[cj2];
-                const double s4v[3] = {s4.x, s4.y, s4.z}, av[3] = {a4.x, a4.y, a4.z}, bv[3] = {b4.x, b4.y, b4.z};
-                double p64[D];
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    double p = P.t[a];
-#pragma unroll
-                    for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
-                    p64[a] = p;
-                }
-                const double da = dist2_exact<D>(av, p64), db = dist2_exact<D>(bv, p64);
-                const bool sw = db < da || (db == da && ob < oa);
-                if (sw) {   // the runner-up is nearer now: the pair relative to it
-                    cpw = pair_code(__uint_as_float(cpw & 0xffff0000u), cj - cj2);
-                    cj = cj2;
-                }
-                // their exact gap now, as a gap relative to cert_pass (the restated certificate subtracts 2 delta
-                // again; the (1 - 1e-6) factors cover the fp32 round trip)
-                const double g = (sqrt(sw ? da : db) - sqrt(sw ? db : da)) * (1.0 - 1e-6) - 1e-12;
-                cgap = (g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f) + 2.f * cdelta;
-                cert = true;
             }
         }
 #ifdef GICP_TIMELINE
@@ -1631,7 +1582,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // certificate: every other target is >= min(runner-up, r(j) - d(p', j)) - e away.
         bool gcert = false;
         float ggap = 0.f;
-        bool peli = false;    // proved at a small gap: find its pair certificate after the descent
 #ifdef GICP_TAIL
         int gwhy = 0;   // diagnostic: how the descent ended for a lane it did not prove
         int gout = 0;   // ... and for one it proved: 1 at the start node's local minimum, 2 at a row entry of
@@ -1642,7 +1592,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 #define GICP_WHY(k) ((void)0)
 #define GICP_OUT(k) ((void)0)
 #endif
-        if (have_jp) cpw = 0u;   // a descending lane's old pair no longer holds (or it had none)
         if (tg.nbq && wave_any(have_jp)) {
             bool act = have_jp;
             int node = jp;
@@ -1759,7 +1708,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         GICP_OUT(h > 0 ? 3 : bk < 0 ? 1 : 2);
                         cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
                         ggap = fminf(e2, r - d0) - e1 - 2.f * e;
-                        peli = A.cert_pair && ggap < A.pair_gap;
                         act = false;
                     } else if (bk < 0) {
                         act = false;                              // local minimum without proof
@@ -1791,26 +1739,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                             p64[a] = p;
                         }
                     }
-                    double bd2 = 1e300, sd2 = 1e300, td2 = 1e300;   // best, runner-up, third
-                    int bj = -1, bo = 0x7fffffff, sj = -1;
+                    double bd2 = 1e300, sd2 = 1e300;
+                    int bj = -1, bo = 0x7fffffff;
                     auto consider = [&](int t) {
                         const double4 t4 = reinterpret_cast<const double4*>(tg.xyz64)[t];
                         const double tv[3] = {t4.x, t4.y, t4.z};
                         const double d2 = dist2_exact<D>(tv, p64);
                         const int og = tg.perm[t];
                         if (d2 < bd2 || (d2 == bd2 && og < bo)) {
-                            td2 = sd2;
                             sd2 = bd2;
-                            sj = bj;
                             bd2 = d2;
                             bj = t;
                             bo = og;
-                        } else if (d2 < sd2) {
-                            td2 = sd2;
-                            sd2 = d2;
-                            sj = t;
                         } else {
-                            td2 = fmin(td2, d2);
+                            sd2 = fmin(sd2, d2);
                         }
                     };
                     consider(tnode);
@@ -1824,58 +1766,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     cj = bj;
                     const double g = (fmin(sqrt(sd2), (double)tfar) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
                     ggap = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
-                    if (A.cert_pair && gcert && sj >= 0) {   // the tie's pair: every other target >= G3 farther
-                        const double g3 = (fmin(sqrt(td2), (double)tfar) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
-                        if (g3 > 2.0 * (double)ggap) cpw = pair_code((float)g3 * (1.0f - 1e-6f), sj - bj);
-                    }
-                }
-            }
-            // a proof at a small runner-up gap: the row again (just read: a cache hit), its candidates' top three
-            // with the loop's arithmetic and order (the same winner), the pair = (winner, runner-up) when the third
-            // (or the row's reach) is clearly farther.  Every target outside {winner, runner-up} lies >= G3 =
-            // min(e3, r - d0) - e1 - 2e farther than the winner (the gap formula of the proof, one rank down).
-            if (wave_any(peli)) {
-                if (peli) {
-                    const uint4* row = tg.nbq + (int64_t)node * 8;
-                    const uint2 hd = reinterpret_cast<const uint2*>(row)[0];
-                    const float r = __uint_as_float(hd.x), sc = __uint_as_float(hd.y);
-                    const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
-                    unsigned u1 = __float_as_uint(d0s), u2 = 0x7f7fffffu, u3 = 0x7f7fffffu;
-                    int k1 = -1, k2 = -2;
-                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
-#pragma unroll
-                    for (int k = 0; k < kGraphK; ++k) {
-                        float c[3];
-#pragma unroll
-                        for (int a = 0; a < 3; ++a) {
-                            const int pp = 4 + 3 * k + a;
-                            const uint32_t wv = rw[pp >> 1];
-                            c[a] = (float)((pp & 1) ? ((int)wv >> 16) : (((int)(wv << 16)) >> 16));
-                        }
-                        const float dx = fmaf(-sc, c[0], qr[0]), dy = fmaf(-sc, c[1], qr[1]), dz = fmaf(-sc, c[2], qr[2]);
-                        const unsigned ud = __float_as_uint(fmaf(dx, dx, fmaf(dy, dy, dz * dz)));
-                        if (ud < u1) {
-                            u3 = u2;
-                            u2 = u1;
-                            k2 = k1;
-                            u1 = ud;
-                            k1 = k;
-                        } else if (ud < u2) {
-                            u3 = u2;
-                            u2 = ud;
-                            k2 = k;
-                        } else {
-                            u3 = min(u3, ud);
-                        }
-                    }
-                    const float d0 = __builtin_amdgcn_sqrtf(d0s);
-                    const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
-                    const float e1 = __builtin_amdgcn_sqrtf(__uint_as_float(u1));
-                    const float g3 = fminf(__builtin_amdgcn_sqrtf(__uint_as_float(u3)), r - d0) - e1 - 2.f * e;
-                    if (k2 >= -1 && g3 > 2.f * ggap) {
-                        const int j2 = k2 < 0 ? node : tg.nbi[(int64_t)node * kGraphK + k2];
-                        cpw = pair_code(g3, j2 - cj);
-                    }
                 }
             }
             if (gcert) {
@@ -2174,10 +2064,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             const Query<D> qa = active_box<D>(q, lb >= 0.f);   // the searching lanes' box
             if (l < nl) {
                 ent = A.list[(int64_t)T * kListMax + l];
-                const TileBox eb = tg.boxes[ent];   // the 48-B record (TileInfo's fields are 144 B apart)
-                eg2 = gap2_box<D>(qa, eb.c, eb.h);
-                est = eb.start;
-                ecnt = eb.count;
+                eg2 = gap2_box<D>(qa, tg.tiles[ent].c, tg.tiles[ent].h);
+                est = tg.tiles[ent].start;
+                ecnt = tg.tiles[ent].count;
             }
             float wb = wave_maxf(lb);
             uint64_t rem = __ballot(l < nl && eg2 <= wb);
@@ -2281,7 +2170,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         } else if (found) {
             const float b = key_d2(best), s2 = key_d2(sec);
             amb = (s2 - b) <= marg(A.mg, b) + marg(A.mg, s2);
-            j = tg.boxes[best_tile].start + (int)(best & 63u);
+            j = tg.tiles[best_tile].start + (int)(best & 63u);
         }
         // Every lane's certificate is restated relative to this pass's pose where the wave walked; a wave
         // that skipped the walk leaves its certificates (and cert_pass) as they are: they stay relative to
@@ -2290,14 +2179,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (A.cert_j && (!skip_walk || any_gcert || A.pass - cpass0 >= kPoseRing / 2)) {
             if (q.valid) {
                 float g = 0.f;
-                uint32_t pw = 0u;   // the pair certificate written with it
                 if (gcert) {
                     g = cgap;   // proved at this pass's pose
-                    pw = cpw;
                 } else if (cert) {
                     g = cj >= 0 ? cgap - 2.f * cdelta : cgap - cdelta;
-                    if (cpw != 0u)   // restated to this pass's pose
-                        pw = pair_code(__uint_as_float(cpw & 0xffff0000u) - 2.f * cdelta, (int)(short)(cpw & 0xffffu));
                 } else if (found) {
                     if (!amb) {   // other targets: scanned >= sec - margin, unscanned > the final bound
                         const float b = key_d2(best), s2 = key_d2(sec);
@@ -2310,7 +2195,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 }
                 A.cert_j[i] = cert ? cj : (found && !amb ? j : -1);
                 A.cert_gap[i] = (found && amb) ? 0.f : g;
-                if (A.cert_pair) A.cert_pair[i] = pw;
             }
             if (l == 0) A.cert_pass[T] = A.pass;
         }
@@ -2382,7 +2266,6 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 const double g = (sqrt((double)fminf(sd2, lim)) - sqrt(bd2)) * (1.0 - 1e-6) - 1e-12;
                 A.cert_j[i] = bj;
                 A.cert_gap[i] = g > 0.0 ? (float)g * (1.0f - 1e-6f) : 0.f;
-                if (A.cert_pair) A.cert_pair[i] = 0u;
             }
         }
 

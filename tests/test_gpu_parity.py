@@ -308,15 +308,13 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
     A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
     default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
-    certificates or lists (plain full walks), one without the target graph's descent, the sparse-wave
-    search off and on for every walking wave, and pair certificates (§3i) off and made for
-    every proof that can have one, while the certified passes evaluate far fewer pairs."""
+    certificates or lists (plain full walks), one without the target graph's descent, and the sparse-wave
+    search off and on for every walking wave, while the certified passes evaluate far fewer
+    pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain", "nopairs", "pairs_all"):
-        monkeypatch.setenv("GICP_NO_PAIRS", "1" if flag == "nopairs" else "0")
-        monkeypatch.setenv("GICP_PAIR_GAP", "1.0" if flag == "pairs_all" else "0.004")
+    for flag in ("0", "1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain"):
         monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "nograph" else "0")
         monkeypatch.setenv("GICP_NO_CERTS", "1" if flag in ("1", "plain", "sparse_all_plain") else "0")
         monkeypatch.setenv("GICP_NO_LISTS", "1" if flag in ("plain", "sparse_all_plain") else "0")
@@ -336,7 +334,7 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    for other in ("1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain", "nopairs", "pairs_all"):
+    for other in ("1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain"):
         assert np.array_equal(out["0"][0], out[other][0]), other
         for a, b in zip(out["0"][1], out[other][1]):
             assert np.array_equal(a, b)
@@ -372,8 +370,7 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
     """Graph descent proves nearest neighbours while the pose still moves by centimetres to decimetres:
     a sequence of passes with growing steps gives bit-identical statistics and correspondence indices with
     and without the graph (GICP_NO_GRAPH=1) and with every walking wave searched lane-parallel
-    (GICP_SPARSE_WALK=64) and with pair certificates for every proof that can have one
-    (GICP_PAIR_GAP=1.0, §3i), and with the graph the moving passes screen fewer pairs."""
+    (GICP_SPARSE_WALK=64), and with the graph the moving passes screen fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, **P3)
     poses = []
@@ -383,10 +380,9 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
         T[:3, 3] = [step, -0.5 * step, 0.25 * step]
         poses.append(T)
     out = {}
-    for flag in ("0", "1", "sparse_all", "pairs_all"):
+    for flag in ("0", "1", "sparse_all"):
         monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "1" else "0")
         monkeypatch.setenv("GICP_SPARSE_WALK", "64" if flag == "sparse_all" else "2")
-        monkeypatch.setenv("GICP_PAIR_GAP", "1.0" if flag == "pairs_all" else "0.004")
         e = gicp.Engine(0)
         try:
             e.set_target(tgt, p)
@@ -399,7 +395,7 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
             out[flag] = (sts, pairs)
         finally:
             e.close()
-    for other in ("1", "sparse_all", "pairs_all"):
+    for other in ("1", "sparse_all"):
         for (a, ia), (b, ib) in zip(out["0"][0], out[other][0]):
             assert np.array_equal(ia, ib) and np.array_equal(a, b), other
     assert sum(out["0"][1][1:]) < sum(out["1"][1][1:])
