@@ -2064,9 +2064,10 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             const Query<D> qa = active_box<D>(q, lb >= 0.f);   // the searching lanes' box
             if (l < nl) {
                 ent = A.list[(int64_t)T * kListMax + l];
-                eg2 = gap2_box<D>(qa, tg.tiles[ent].c, tg.tiles[ent].h);
-                est = tg.tiles[ent].start;
-                ecnt = tg.tiles[ent].count;
+                const TileBox eb = tg.boxes[ent];   // the 48-B record (TileInfo's fields are 144 B apart)
+                eg2 = gap2_box<D>(qa, eb.c, eb.h);
+                est = eb.start;
+                ecnt = eb.count;
             }
             float wb = wave_maxf(lb);
             uint64_t rem = __ballot(l < nl && eg2 <= wb);
@@ -2170,7 +2171,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         } else if (found) {
             const float b = key_d2(best), s2 = key_d2(sec);
             amb = (s2 - b) <= marg(A.mg, b) + marg(A.mg, s2);
-            j = tg.tiles[best_tile].start + (int)(best & 63u);
+            j = tg.boxes[best_tile].start + (int)(best & 63u);
         }
         // Every lane's certificate is restated relative to this pass's pose where the wave walked; a wave
         // that skipped the walk leaves its certificates (and cert_pass) as they are: they stay relative to
