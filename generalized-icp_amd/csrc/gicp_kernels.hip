@@ -1840,8 +1840,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             return r * r;
         };
         float lbx = inflate(lb);
+        // lane k: list entry k once the list walk has visited it; a full walk that continues a list walk
+        // whose certificate failed skips those tiles (their rows are already in every lane's best and
+        // runner-up; -1 elsewhere, so no other walk skips anything)
+        int lvis = -1;
         // visit target tile Tt; `pre` = its coordinates already loaded (prefetch) or null
         auto visit_pre = [&](int Tt, const float4* pre) -> bool {
+            if (wave_any(lvis == Tt)) return false;
             S.mark(1);
             S.count(0);
             const TileInfo ti = tile_meta(tg, Tt);
@@ -2086,6 +2091,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     wb = wave_maxf(lb);
                     rem &= __ballot(eg2 <= wb);
                 }
+                if (l == k) lvis = ent;
                 if (kn >= 0 && ((rem >> kn) & 1ull)) {
                     k = kn;
                     pv = pvn;
@@ -2096,12 +2102,11 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
             const float wbf = wave_maxf(lb);
             if (__builtin_amdgcn_sqrtf(fmaxf(wbf, 0.f)) * 1.0001f + delta > rc) {
-                // not certified: start over with the full walk (and rebuild the list)
+                // not certified: the full walk (which rebuilds the list) continues from the list walk's
+                // best, runner-up and bounds and skips the tiles the list walk visited: each lane's result
+                // is still the minimum over every row within its final bound, and a row never scanned
+                // lies beyond the bound its tile or sub-tile was tested against, which only shrank
                 use = false;
-                best = sec = init;
-                best_tile = -1;
-                lb = lane_bound();
-                lbx = inflate(lb);
                 ++list_rebuilds;
             }
         }
@@ -2257,7 +2262,12 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     visit64(__builtin_amdgcn_readlane(ent, k));
                 }
             } else {
-                traverse<D>(tg, q, seed, visit64, [&]() { return wave_maxf(amb ? lim : -1.f); });  // seed: wave-uniform
+                // candidate tiles against the box of the re-resolved lanes only (not the whole source
+                // tile's), found as the full walk finds them (TileBox records, one round trip per level);
+                // visit64's per-lane test decides what is scanned, so the result does not depend on it
+                const Query<D> qb = active_box<D>(q, amb);
+                walk_c<D>(tg, qb, seed, [&](int Tt, const float4*) { return visit64(Tt); },
+                          [&]() { return wave_maxf(amb ? lim : -1.f); }, 0.f, [](int) {});
             }
             if (amb) j = bj;
             // exact certificate of a re-resolved lane: every row within lim was scanned in fp64, so

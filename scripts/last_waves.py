@@ -119,12 +119,24 @@ def main():
             print(f"  sparse waves n {sp.sum()}: walk {np.mean(w['ph'][3][sp]):5.2f} us, walkers covered by the list"
                   f" {np.mean(w['list_used'][sp]):4.2f} / wave, candidate super-blocks {np.mean(w['blk'][sp]):4.2f} / wave,"
                   f" tiles screened {np.mean(w['visits'][sp]):5.1f} / wave")
+        fb = w["fb"] > 0   # waves with an fp64 re-resolution (its visits are inside epi_ld)
+        if fb.any():
+            epi = w["ph"][4]
+            # what-if bounds (queueing ignored): the pass's span with each such wave's epi_ld cut to 3 us, and
+            # with each walk of > 10 visits halved
+            cut = np.where(fb, np.maximum(epi - 3.0, 0.0), 0.0)
+            half = np.where(w["visits"] > 10, 0.5 * w["ph"][3], 0.0)
+            print(f"  fp64 re-resolution: waves {fb.sum()} (last 1%: {(fb & last1).sum()}), epi_ld {np.mean(epi[fb]):5.1f} us"
+                  f" (others {np.mean(epi[~fb]):4.1f}), fp64 visits {np.mean(w['fb'][fb]):4.1f} / wave;"
+                  f" span if <= 3 us {np.max(end - cut):6.1f}, if long walks halved {np.max(end - half):6.1f},"
+                  f" both {np.max(end - cut - half):6.1f}")
         print(describe(w, last1, "last 1%"))
         for i in order[:6]:
             phs = " ".join(f"{w['ph'][j, i]:4.1f}" for j in range(len(PH)))
             print(f"    tile {w['tile'][i]:6d} xcc {w['xcc'][i]} start {w['start'][i]:6.1f} end {w['end'][i]:6.1f} [{phs}]"
                   f" {KIND[int(w['kind'][i])]}: {w['visits'][i]} visits, {w['scanned'][i]} scanned, {w['nwalk'][i]} walkers"
-                  f" ({w['nwalk_jp'][i]} with a last match), radius {w['wb0'][i]:.3f}, {w['ndesc'][i]} descended")
+                  f" ({w['nwalk_jp'][i]} with a last match), radius {w['wb0'][i]:.3f}, {w['ndesc'][i]} descended,"
+                  f" {w['fb'][i]} fp64 visits")
     for f in os.listdir(tmp):
         os.remove(os.path.join(tmp, f))
     os.rmdir(tmp)
