@@ -339,6 +339,7 @@ struct gicp_ctx {
     int src_tile = kTile;             // source points per tile at most: 64, 32 or 16 (GICP_SRC_TILE)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
     int sparse_max = 2;               // CorrArgs::sparse_max (GICP_SPARSE_WALK; 0: sparse waves walk like the rest)
+    int sparse_amb = 2;               // CorrArgs::sparse_amb (GICP_SPARSE_AMB; 0: every fp64 re-resolution wave-wide)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
     BuildScratch bs;
@@ -902,6 +903,7 @@ CorrArgs corr_args(gicp_ctx* c, int single_pass) {
     a.pass = ++c->pass;
     a.use_lists = c->use_lists ? 1 : 0;
     a.sparse_max = c->sparse_max;
+    a.sparse_amb = c->sparse_amb;
     a.skin = (float)(c->skin_frac * dc);
     a.skin_gain = (float)c->skin_gain;
     a.skin_max = (float)dc;
@@ -1174,6 +1176,7 @@ int gicp_create(gicp_ctx** out, int device) {
     }
     if (const char* e = std::getenv("GICP_CERT_KAPPA")) c->kappa_frac = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("GICP_SPARSE_WALK")) c->sparse_max = std::max(0, std::min(64, std::atoi(e)));
+    if (const char* e = std::getenv("GICP_SPARSE_AMB")) c->sparse_amb = std::max(0, std::min(64, std::atoi(e)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         delete c;

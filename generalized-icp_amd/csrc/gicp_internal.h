@@ -258,6 +258,10 @@ struct CorrArgs {
     // a wave with 1 .. sparse_max walking lanes searches lane-parallel, one walking lane at a time (the candidate
     // tiles' rows kSparseGroup tiles per memory round trip) instead of one visit per tile; 0: never
     int32_t sparse_max;
+    // a wave with 1 .. sparse_amb lanes the fp32 screen left ambiguous re-resolves them lane-parallel, one at a
+    // time (its candidate tiles from the box hierarchy, a tile's rows one per lane, exact fp64), else wave-wide
+    // with a walk (GICP_SPARSE_AMB; 0: always wave-wide)
+    int32_t sparse_amb;
     float skin;
     // a tile rebuilding its list while the pose still moves uses skin' = min(max(skin, skin_gain x its
     // displacement over the last pass), skin_max): the list then outlasts a step of the same size

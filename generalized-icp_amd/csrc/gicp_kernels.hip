@@ -1466,7 +1466,14 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         if (done) return;
         Query<D> q;
         q.valid = l < st.count;
-        const int i = st.start + min(l, st.count - 1);
+        int i = st.start + min(l, st.count - 1);
+        // the point's index again where the epilogue needs it: recomputed from the tile's scalars (an empty
+        // asm keeps the compiler from carrying the first copy, and its 64-bit address, through the search's
+        // register peak, where it was spilled to scratch)
+        auto refresh_i = [&]() {
+            i = st.start + min(lane_id(), st.count - 1);
+            asm volatile("" : "+v"(i));
+        };
         const float4 rel = sc.rel32[i];
         const float relv[3] = {rel.x, rel.y, rel.z};
 #pragma unroll
@@ -2156,18 +2163,23 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // the fp64 source point is needed only from here on (kept out of the walk's registers).  A wave
         // that walked needs it now (fp64 fallback); one that skipped the walk requests it with its
         // matches and covariances in the epilogue: one memory round trip instead of two
-        auto source_point = [&](const double4& s4) {
+        // (the untransformed point sv, a statistics term, is taken again from the epilogue's own request of it:
+        // held from here it was spilled through the fp64 re-resolution)
+        auto source_point = [&](const double4& s4, bool p64) {
             const double s4v[3] = {s4.x, s4.y, s4.z};
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                double p = P.t[a];
+                if (p64) {
+                    double p = P.t[a];
 #pragma unroll
-                for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
-                q.p64[a] = p;
+                    for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
+                    q.p64[a] = p;
+                }
                 sv[a] = s4v[a];
             }
         };
-        if (!skip_walk) source_point(reinterpret_cast<const double4*>(sc.xyz64)[i]);
+        refresh_i();
+        if (!skip_walk) source_point(reinterpret_cast<const double4*>(sc.xyz64)[i], true);
         const bool found = cert ? cj >= 0 : (q.valid && best < init);
         int j = -1;
         double d2e = 0.0;
@@ -2250,7 +2262,98 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 wave_sync();
                 return true;
             };
-            if (use) {   // the certified candidate list covers every tile within lb >= lim
+            const uint64_t am = __ballot(amb);
+            if (__popcll(am) <= A.sparse_amb) {
+                // few re-resolved lanes (the usual case): for one at a time, its candidate tiles -- every tile
+                // whose box lies within lim of the lane's point, from the super-block / block / tile boxes as the
+                // sparse search finds them -- are screened exactly with lane r holding row r of a tile (one
+                // memory round trip per tile, no staging, no row loop), the tile's nearest by the tie
+                // rule and its runner-up taken over the wave.  Same nearest as visit64 (the exact minimum over
+                // a superset of the rows within lim, ties to the smaller original index); the runner-up may
+                // also count rows beyond lim, which only the (sound) certificate gap sees.
+                uint64_t wm = am;
+                while (wm) {
+                    const int wl = __ffsll((unsigned long long)wm) - 1;
+                    wm &= wm - 1;
+                    double pa[3] = {0.0, 0.0, 0.0};
+                    Query<D> qp = q;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) {
+                        pa[a] = readlane_d(q.p64[a], wl);
+                        const float pw = readlane_f(q.pw[a], wl);
+                        const float B = 2.f * q.ew[a] + 1e-30f;
+                        qp.ow[a] = q.ow[a] + (double)pw;
+                        qp.ew[a] = 4.8e-7f * (2.f * fabsf(pw) + B) + 1e-30f;
+                    }
+                    const float limw = readlane_f(lim, wl);
+                    double ub = 1e300;            // the lane's exact best d^2 so far (uniform) ...
+                    int uo = 0x7fffffff, uj = -1; // ... its original and sorted index
+                    float us = 3e38f;             // ... and the runner-up, rounded down as visit64 rounds it
+                    // the tiles of the lanes in cm (lane k: start ts, count tc), one per round trip
+                    auto screen64 = [&](uint64_t cm, int ts, int tc) {
+                        while (cm) {
+                            const int k = __ffsll((unsigned long long)cm) - 1;
+                            cm &= cm - 1;
+                            const int s0 = __builtin_amdgcn_readlane(ts, k), c0 = __builtin_amdgcn_readlane(tc, k);
+                            S.count(7);
+                            double d2 = 1e300;
+                            int og = 0x7fffffff;
+                            if (l < c0) {
+                                const double4 x = reinterpret_cast<const double4*>(tg.xyz64)[s0 + l];
+                                og = tg.perm[s0 + l];
+                                const double xv[3] = {x.x, x.y, x.z};
+                                d2 = dist2_exact<D>(xv, pa);
+                            }
+                            const double m = wave_mind(d2);
+                            const uint64_t eq = __ballot(d2 == m);
+                            const int om = (int)wave_min_key(d2 == m ? (unsigned)og : 0x7fffffffu);
+                            const int wn = __ffsll((unsigned long long)__ballot(d2 == m && og == om)) - 1;
+                            const double st = __popcll(eq) >= 2 ? m : wave_mind(l == wn ? 1e300 : d2);
+                            if (m < ub || (m == ub && om < uo)) {
+                                us = fminf(us, fminf((float)ub * 0.99999976f, (float)st * 0.99999976f));
+                                ub = m;
+                                uo = om;
+                                uj = s0 + wn;
+                            } else {
+                                us = fminf(us, (float)m * 0.99999976f);
+                            }
+                        }
+                    };
+                    const int nsuper = (tg.nblocks + kWave - 1) / kWave;
+                    for (int s0 = 0; s0 < nsuper; s0 += kWave) {
+                        float sg = 3e38f;
+                        if (s0 + l < nsuper) sg = gap2_box<D>(qp, tg.blocks[tg.nblocks + s0 + l].c, tg.blocks[tg.nblocks + s0 + l].h);
+                        uint64_t sm = __ballot(sg <= limw);
+                        while (sm) {
+                            const int sl = __ffsll((unsigned long long)sm) - 1;
+                            sm &= sm - 1;
+                            const int b0 = (s0 + sl) * kWave, b = b0 + l;
+                            float bg = 3e38f;
+                            if (b < tg.nblocks) bg = gap2_box<D>(qp, tg.blocks[b].c, tg.blocks[b].h);
+                            uint64_t bm = __ballot(bg <= limw);
+                            while (bm) {
+                                const int bl = __ffsll((unsigned long long)bm) - 1;
+                                bm &= bm - 1;
+                                const int first = (b0 + bl) * kBlockTiles, nt = min(kBlockTiles, tg.ntiles - first);
+                                int hst = 0, hcn = 0;
+                                float hg = 3e38f;
+                                if (l < nt) {
+                                    const TileBox tbx = tg.boxes[first + l];
+                                    hg = gap2_box<D>(qp, tbx.c, tbx.h);
+                                    hst = tbx.start;
+                                    hcn = tbx.count;
+                                }
+                                screen64(__ballot(l < nt && hg <= limw), hst, hcn);
+                            }
+                        }
+                    }
+                    if (l == wl) {
+                        bd2 = ub;
+                        sd2 = us;
+                        bj = uj;
+                    }
+                }
+            } else if (use) {   // the certified candidate list covers every tile within lb >= lim
                 const Query<D> qb = active_box<D>(q, amb);   // entries near the re-resolved lanes only
                 bool near = false;
                 const float limw = wave_maxf(amb ? lim : -1.f);
@@ -2282,14 +2385,13 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
 
         S.mark(4);
         // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
-        double4 s4e = make_double4(0.0, 0.0, 0.0, 0.0);
-        if (skip_walk) s4e = reinterpret_cast<const double4*>(sc.xyz64)[i];
+        const double4 s4e = reinterpret_cast<const double4*>(sc.xyz64)[i];
         if (found && j >= 0) {
             // match position and both covariances requested together (one memory round trip)
             const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
             const double4 ct = tg.cov[j];
             const double4 cs = sc.cov[i];
-            if (skip_walk) source_point(s4e);
+            source_point(s4e, skip_walk);
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
 #ifdef GICP_TIMELINE
@@ -2366,7 +2468,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = on ? (int64_t)tg.perm[j] : -1;
         } else if (q.valid) {
-            if (skip_walk) source_point(s4e);
+            source_point(s4e, skip_walk);
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = -1;
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = 1.0 / 0.0;
         }

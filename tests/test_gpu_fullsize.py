@@ -93,7 +93,8 @@ def test_align_1m_properties(eng, scene1m):
     # without certificates (and their search cap), then also without candidate lists: same poses, bit for bit
     for env in ({"GICP_NO_GRAPH": "1"}, {"GICP_NO_CERTS": "1"}, {"GICP_NO_CERTS": "1", "GICP_NO_LISTS": "1"},
                 {"GICP_MOVING_ITERS": "0"}, {"GICP_MOVING_ITERS": "0", "GICP_UNIT_MAP": "1"},
-                {"GICP_MOVING_ITERS": "30", "GICP_MOVING_MAP": "3"}, {"GICP_SPARSE_WALK": "0"}, {"GICP_SPARSE_WALK": "8"}):
+                {"GICP_MOVING_ITERS": "30", "GICP_MOVING_MAP": "3"}, {"GICP_SPARSE_WALK": "0"}, {"GICP_SPARSE_WALK": "8"},
+                {"GICP_SPARSE_AMB": "0"}, {"GICP_SPARSE_AMB": "64"}):
         os.environ.update(env)
         try:
             e2 = gicp.Engine(0)

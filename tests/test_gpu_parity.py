@@ -308,14 +308,16 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
     candidate lists (adaptive skin) and the super-block level only change which tiles a walk tests.
     A 60-iteration fixed run and single passes around its endpoint must be bit-identical across the
     default engine, one without certificates (GICP_NO_CERTS=1, no cap either) and one without
-    certificates or lists (plain full walks), one without the target graph's descent, and the sparse-wave
-    search off and on for every walking wave, while the certified passes evaluate far fewer
-    pairs."""
+    certificates or lists (plain full walks), one without the target graph's descent, the sparse-wave
+    search off and on for every walking wave, and the lane-parallel fp64 re-resolution
+    (GICP_SPARSE_AMB) off and on for every wave with an ambiguous lane, while the certified passes evaluate
+    far fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, fixed_iterations=1, max_iterations=60, **P3)
     out = {}
-    for flag in ("0", "1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain"):
+    for flag in ("0", "1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain", "amb_off", "amb_all"):
         monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "nograph" else "0")
+        monkeypatch.setenv("GICP_SPARSE_AMB", "0" if flag == "amb_off" else "64" if flag == "amb_all" else "2")
         monkeypatch.setenv("GICP_NO_CERTS", "1" if flag in ("1", "plain", "sparse_all_plain") else "0")
         monkeypatch.setenv("GICP_NO_LISTS", "1" if flag in ("plain", "sparse_all_plain") else "0")
         monkeypatch.setenv("GICP_SPARSE_WALK", "0" if flag == "sparse_off" else "64" if flag.startswith("sparse_all") else "2")
@@ -334,7 +336,7 @@ def test_nn_certificates_do_not_change_results(scene3d, monkeypatch):
             out[flag] = (T, sts, e.pass_info()["pairs"], r["pairs_evaluated"])
         finally:
             e.close()
-    for other in ("1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain"):
+    for other in ("1", "plain", "nograph", "sparse_off", "sparse_all", "sparse_all_plain", "amb_off", "amb_all"):
         assert np.array_equal(out["0"][0], out[other][0]), other
         for a, b in zip(out["0"][1], out[other][1]):
             assert np.array_equal(a, b)
@@ -370,7 +372,8 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
     """Graph descent proves nearest neighbours while the pose still moves by centimetres to decimetres:
     a sequence of passes with growing steps gives bit-identical statistics and correspondence indices with
     and without the graph (GICP_NO_GRAPH=1) and with every walking wave searched lane-parallel
-    (GICP_SPARSE_WALK=64), and with the graph the moving passes screen fewer pairs."""
+    (GICP_SPARSE_WALK=64) or every ambiguous lane re-resolved wave-wide (GICP_SPARSE_AMB=0),
+    and with the graph the moving passes screen fewer pairs."""
     src, tgt, _ = scene3d
     p = gicp.default_params(3, **P3)
     poses = []
@@ -380,9 +383,10 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
         T[:3, 3] = [step, -0.5 * step, 0.25 * step]
         poses.append(T)
     out = {}
-    for flag in ("0", "1", "sparse_all"):
+    for flag in ("0", "1", "sparse_all", "amb_off"):
         monkeypatch.setenv("GICP_NO_GRAPH", "1" if flag == "1" else "0")
         monkeypatch.setenv("GICP_SPARSE_WALK", "64" if flag == "sparse_all" else "2")
+        monkeypatch.setenv("GICP_SPARSE_AMB", "0" if flag == "amb_off" else "2")
         e = gicp.Engine(0)
         try:
             e.set_target(tgt, p)
@@ -395,7 +399,7 @@ def test_graph_descent_along_a_moving_pose(scene3d, monkeypatch):
             out[flag] = (sts, pairs)
         finally:
             e.close()
-    for other in ("1", "sparse_all"):
+    for other in ("1", "sparse_all", "amb_off"):
         for (a, ia), (b, ib) in zip(out["0"][0], out[other][0]):
             assert np.array_equal(ia, ib) and np.array_equal(a, b), other
     assert sum(out["0"][1][1:]) < sum(out["1"][1][1:])
