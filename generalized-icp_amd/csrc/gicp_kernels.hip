@@ -2163,23 +2163,20 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         // the fp64 source point is needed only from here on (kept out of the walk's registers).  A wave
         // that walked needs it now (fp64 fallback); one that skipped the walk requests it with its
         // matches and covariances in the epilogue: one memory round trip instead of two
-        // (the untransformed point sv, a statistics term, is taken again from the epilogue's own request of it:
-        // held from here it was spilled through the fp64 re-resolution)
-        auto source_point = [&](const double4& s4, bool p64) {
+        // the transformed point q.p64 (the untransformed one, sv, a statistics term, is set from the epilogue's
+        // own request of the point: held from here it was spilled through the fp64 re-resolution)
+        auto source_point = [&](const double4& s4) {
             const double s4v[3] = {s4.x, s4.y, s4.z};
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                if (p64) {
-                    double p = P.t[a];
+                double p = P.t[a];
 #pragma unroll
-                    for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
-                    q.p64[a] = p;
-                }
-                sv[a] = s4v[a];
+                for (int b = 0; b < D; ++b) p += P.R[a * D + b] * s4v[b];
+                q.p64[a] = p;
             }
         };
         refresh_i();
-        if (!skip_walk) source_point(reinterpret_cast<const double4*>(sc.xyz64)[i], true);
+        if (!skip_walk) source_point(reinterpret_cast<const double4*>(sc.xyz64)[i]);
         const bool found = cert ? cj >= 0 : (q.valid && best < init);
         int j = -1;
         double d2e = 0.0;
@@ -2386,12 +2383,15 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
         S.mark(4);
         // ---- epilogue: distance check, W = inv(R C_s R^T + C_t), statistics --
         const double4 s4e = reinterpret_cast<const double4*>(sc.xyz64)[i];
+        sv[0] = s4e.x;
+        sv[1] = s4e.y;
+        if (D == 3) sv[D - 1] = s4e.z;
         if (found && j >= 0) {
             // match position and both covariances requested together (one memory round trip)
             const double4 q4 = reinterpret_cast<const double4*>(tg.xyz64)[j];
             const double4 ct = tg.cov[j];
             const double4 cs = sc.cov[i];
-            source_point(s4e, skip_walk);
+            if (skip_walk) source_point(s4e);
             const double qv[3] = {q4.x, q4.y, q4.z};
             d2e = dist2_exact<D>(qv, q.p64);
 #ifdef GICP_TIMELINE
@@ -2468,7 +2468,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             }
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = on ? (int64_t)tg.perm[j] : -1;
         } else if (q.valid) {
-            source_point(s4e, skip_walk);
+            if (skip_walk) source_point(s4e);
             if (A.dbg_index) A.dbg_index[sc.perm[i]] = -1;
             if (A.dbg_dist) A.dbg_dist[sc.perm[i]] = 1.0 / 0.0;
         }
