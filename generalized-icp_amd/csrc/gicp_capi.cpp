@@ -182,14 +182,15 @@ struct Cloud {
     TileBox* boxes = nullptr;         // the walk's compact tile records (k_build_tiles)
     int32_t* seed_tab = nullptr;      // Morton seed lookup (DevCloud::seed_tab), built on the host
     int seed_shift = 0;
-    uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows
+    uint4* nbq = nullptr;             // neighbour graph (targets only): packed rows (line A)
+    uint4* nbx = nullptr;             // ... their last entries
     int32_t* nbi = nullptr;           // ... and their sorted indices
     bool graph_ready = false;
     bool cov_ready = false;
     int cov_shard = 0, cov_nshards = 1;  // whose tiles' covariances were computed (build_cloud)
 
     size_t cap_xyz = 0, cap_rel = 0, cap_cov = 0, cap_perm = 0, cap_inv = 0, cap_cnt = 0;
-    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbi = 0, cap_boxes = 0, cap_seed = 0;
+    size_t cap_tiles = 0, cap_blocks = 0, cap_tcode = 0, cap_nbq = 0, cap_nbx = 0, cap_nbi = 0, cap_boxes = 0, cap_seed = 0;
     void reserve_points(int64_t np) {
         dreserve(xyz64, cap_xyz, (size_t)np * 4);
         dreserve(rel32, cap_rel, (size_t)np);
@@ -217,9 +218,10 @@ struct Cloud {
         dfree(boxes);
         dfree(seed_tab);
         dfree(nbq);
+        dfree(nbx);
         dfree(nbi);
         cap_xyz = cap_rel = cap_cov = cap_perm = cap_inv = cap_cnt = cap_tiles = cap_blocks = cap_tcode = 0;
-        cap_nbq = cap_nbi = cap_boxes = cap_seed = 0;
+        cap_nbq = cap_nbx = cap_nbi = cap_boxes = cap_seed = 0;
         n = 0;
         cov_ready = false;
         graph_ready = false;
@@ -237,6 +239,7 @@ struct Cloud {
         v.seed_tab = seed_tab;
         v.seed_shift = seed_shift;
         v.nbq = graph_ready ? nbq : nullptr;
+        v.nbx = graph_ready ? nbx : nullptr;
         v.nbi = graph_ready ? nbi : nullptr;
         v.n = n;
         v.ntiles = ntiles;
@@ -770,6 +773,7 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
         GraphArgs ga{};
         if (graph) {
             dreserve(cl.nbq, cl.cap_nbq, (size_t)n * 8);
+            dreserve(cl.nbx, cl.cap_nbx, (size_t)n * 3);
             dreserve(cl.nbi, cl.cap_nbi, (size_t)n * kGraphK);
             dreserve(bs.g_nb, bs.cap_gnb, (size_t)n * kGraphK);   // unpacked rows (scratch)
             dreserve(bs.g_nbh, bs.cap_gnbh, (size_t)n);
@@ -780,6 +784,7 @@ void build_cloud(Cloud& cl, const double* xyz, int64_t n, int dim, const gicp_pa
             ga.nb = bs.g_nb;
             ga.nbh = bs.g_nbh;
             ga.nbq = cl.nbq;
+            ga.nbx = cl.nbx;
             ga.nbi = cl.nbi;
             ca.g_nb = bs.g_nb;
             ca.g_nbh = bs.g_nbh;

@@ -42,6 +42,13 @@ constexpr int kGraphHops = GICP_GRAPH_HOPS;   // descent steps a k_corr lane may
 // error bound of the descent's fp32 distances, per metre of the coordinates involved (2^-19: the
 // relative-to-node arithmetic errs by a few 2^-24 per operation)
 constexpr float kGraphErr = 1.9073486328125e-06f;
+// graph row layout (DevCloud::nbq / nbx): entries per 128-B line and per first half-line, and the index delta
+// that marks an entry whose sorted-index delta does not fit 16 bits
+constexpr int kGraphLineA = 15;
+constexpr int kGraphHalf = 7;
+constexpr int kGraphFar = -32768;
+static_assert(2 + 2 * kGraphLineA == 32 && 2 + 2 * kGraphHalf == 16, "header + entries fill the line and its half");
+static_assert(2 * (kGraphK - kGraphLineA) == 10, "the remaining entries fill 40 B of the 48-B record");
 
 struct __attribute__((aligned(16))) TileInfo {
     double c[3];      // fp64 centre (midpoint of the fp64 AABB)
@@ -87,12 +94,15 @@ struct DevCloud {
     // [seed_tab[c >> seed_shift], seed_tab[(c >> seed_shift) + 1]] (a few binary steps instead of log2 ntiles)
     const int32_t* seed_tab;
     int32_t seed_shift;
-    // neighbour graph (target only; null when not built), DESIGN.md §3c.  Row i is one 128-B line:
-    // dword 0 r(i) (fp32: every target t != i with |x_t - x_i| < r is in the row), dword 1 the scale s,
-    // then kGraphK entries of 3 int16 (x_t - x_i) / s, rounded to nearest (|error| <= s / 2 per
-    // axis); an unused entry repeats the last real one (offset 0 in an empty row).  nbi[i][k] = sorted index of
-    // entry k (-1 unused).
+    // neighbour graph (target only; null when not built), DESIGN.md §3c.  Row i: dword 0 r(i) (fp32: every
+    // target t != i with |x_t - x_i| < r is in the row), dword 1 the scale s, then kGraphK entries nearest-first,
+    // two dwords each: (x_t - x_i) / s as 3 int16 rounded to nearest (|error| <= s / 2 per axis) and the
+    // sorted-index delta t - i as a fourth int16 (kGraphFar when it does not fit: nbi holds it), so a descent
+    // step needs no index read.  Entries 0 .. kGraphLineA - 1 fill the 128-B line nbq[i] (its first half holds
+    // the header and entries 0 .. kGraphHalf - 1), the rest the 48-B record nbx[i].  An unused entry repeats
+    // the last real one (offset and delta 0 in an empty row).  nbi[i][k] = sorted index of entry k (-1 unused).
     const uint4* nbq;         // [n][8]
+    const uint4* nbx;         // [n][3]
     const int32_t* nbi;       // [n][kGraphK]
     int64_t n;
     int32_t ntiles;
@@ -115,10 +125,10 @@ struct GraphArgs {
     Margin mg;
     float4* nb;               // [n][kGraphK] scratch: x_t - x_i fp32, t as the w bits
     float2* nbh;              // [n] scratch: (r, count)
-    uint4* nbq;               // [n][8] out (packed rows)
+    uint4* nbq;               // [n][8] out (packed rows: header and entries 0 .. kGraphLineA - 1)
+    uint4* nbx;               // [n][3] out (entries kGraphLineA .. kGraphK - 1)
     int32_t* nbi;             // [n][kGraphK] out
 };
-static_assert(8 + 6 * kGraphK <= 128, "a graph row is one 128-B line");
 
 struct CovArgs {
     DevCloud cl;

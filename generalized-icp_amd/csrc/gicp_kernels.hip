@@ -1154,11 +1154,13 @@ __global__ void __launch_bounds__(256) k_knn_cov(CovArgs A) {
 // key > tau, so its true d2 >= key_d2(lk[kGraphK + 1]) - margin when that key is above tau (else
 // key_d2(tau) - margin); a lane that found fewer keys within the screen radius has every target within it:
 // r2 = search2 - margin.
-// Pack the graph rows into one 128-B line each (GraphArgs / DevCloud::nbq): offsets quantised to
-// int16 in units of s = max |offset| / 32767 (error <= s / 2 per axis, which k_corr's bound adds),
-// entries ordered nearest-first.
+// Pack the graph rows (DevCloud::nbq / nbx): offsets quantised to int16 in units of s = max |offset| / 32767
+// (error <= s / 2 per axis, which k_corr's bound adds), entries ordered nearest-first, each with its
+// sorted-index delta (kGraphFar when it does not fit 16 bits), so a descent step finds the next node without
+// reading nbi.
 __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ nb, const float2* __restrict__ nbh,
-                                                    int64_t n, uint4* __restrict__ nbq, int32_t* __restrict__ nbi) {
+                                                    int64_t n, uint4* __restrict__ nbq, uint4* __restrict__ nbx,
+                                                    int32_t* __restrict__ nbi) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float2 h = nbh[i];
@@ -1170,8 +1172,8 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
     }
     const float s = m > 0.f ? m / 32767.f : 1e-30f;
     const float inv = 1.f / s;
-    // entries nearest-first (squared offset length, ties by sorted index): k_corr's descent reads a row's
-    // first half and needs the second only when an entry there could still be the nearest
+    // entries nearest-first (squared offset length, ties by sorted index): k_corr's descent reads the first
+    // half-line and needs the rest only when an entry there could still be the nearest
     float key[kGraphK];
     int ord[kGraphK];
     for (int k = 0; k < cnt; ++k) {
@@ -1187,28 +1189,32 @@ __global__ void __launch_bounds__(256) k_graph_pack(const float4* __restrict__ n
         key[pos] = kk;
         ord[pos] = k;
     }
-    uint32_t w[32];
+    uint32_t w[2 + 2 * kGraphK];
     w[0] = __float_as_uint(h.x);
     w[1] = __float_as_uint(s);
-    int16_t* e = reinterpret_cast<int16_t*>(w + 2);
-    // unused entries (k >= cnt) repeat the last real entry (or the node itself, offset 0, in an empty
-    // row), so the descent needs no per-entry validity test: a repeated entry never becomes the
+    // unused entries (k >= cnt) repeat the last real entry (or the node itself, offset and delta 0, in an
+    // empty row), so the descent needs no per-entry validity test: a repeated entry never becomes the
     // strictly nearer candidate and at most makes the runner-up equal the winner, which the descent
     // treats as a near tie resolved exactly over the real entries (nbi = -1 marks the repeats)
-    int16_t q[3] = {0, 0, 0};
+    int q[4] = {0, 0, 0, 0};
     for (int k = 0; k < kGraphK; ++k) {
         int idx = -1;
         if (k < cnt) {
             const float4 v = nb[i * kGraphK + ord[k]];
             const float c[3] = {v.x, v.y, v.z};
-            for (int a = 0; a < 3; ++a) q[a] = (int16_t)max(-32767, min(32767, __float2int_rn(c[a] * inv)));
+            for (int a = 0; a < 3; ++a) q[a] = max(-32767, min(32767, __float2int_rn(c[a] * inv)));
             idx = __float_as_int(v.w);
+            const int64_t d = (int64_t)idx - i;
+            q[3] = d >= -32767 && d <= 32767 ? (int)d : kGraphFar;
         }
-        for (int a = 0; a < 3; ++a) e[3 * k + a] = q[a];
+        w[2 + 2 * k] = ((uint32_t)q[0] & 0xFFFFu) | ((uint32_t)q[1] << 16);
+        w[3 + 2 * k] = ((uint32_t)q[2] & 0xFFFFu) | ((uint32_t)q[3] << 16);
         nbi[i * kGraphK + k] = idx;
     }
-    for (int k = 2 + (3 * kGraphK + 1) / 2; k < 32; ++k) w[k] = 0u;
     for (int c = 0; c < 8; ++c) nbq[i * 8 + c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+    uint32_t x[12] = {};
+    for (int k = 0; k < 2 * (kGraphK - kGraphLineA); ++k) x[k] = w[2 + 2 * kGraphLineA + k];
+    for (int c = 0; c < 3; ++c) nbx[i * 3 + c] = make_uint4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1263,14 +1269,10 @@ __device__ __forceinline__ double stat_value(int k, const double (&W)[D][D], con
     return 1.0;
 }
 
-#ifndef GICP_ROW_SPLIT
-#define GICP_ROW_SPLIT 9
-#endif
 #ifndef GICP_SPARSE_GROUP
 #define GICP_SPARSE_GROUP 4
 #endif
 constexpr int kSparseGroup = GICP_SPARSE_GROUP;   // candidate tiles per round trip of a sparse wave's search
-constexpr int kRowSplit = GICP_ROW_SPLIT;   // graph descent: the row's second half is requested before entry kRowSplit (<= 9)
 
 // In-kernel exchange of a workgroup's NV values with every peer rank (PeerArgs, gicp_internal.h), called by
 // all threads of one workgroup: `vals` (LDS) goes into this rank's slot of every rank's area, then the
@@ -1544,6 +1546,9 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
             jp = A.cert_j[i];
             const float g0 = A.cert_gap[i];
             cdelta = disp_since(cpass0);
+            // (wave-uniform: in 3-D held in a scalar register through the descent and walk -- a vector one was
+            // spilled there; the 2-D kernel allocates better without)
+            if constexpr (D == 3) cdelta = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cdelta)));
             if (cdelta >= 0.f && q.valid) {
                 cj = jp;
                 cgap = g0;
@@ -1612,7 +1617,8 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                 if (act) {
                     uint32_t w[32];
                     const uint4* row = tg.nbq + (int64_t)node * 8;
-                    // the line in two halves (entries 0-8 need dwords 0-15): half the registers live
+                    // the line in two halves (header + entries 0 .. kGraphHalf - 1, then the rest of line A):
+                    // half the registers live
                     auto load_half = [&](int c0) {
 #pragma unroll
                         for (int c = c0; c < c0 + 4; ++c) {
@@ -1631,27 +1637,37 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     }
                     const float r = __uint_as_float(w[0]), sc = __uint_as_float(w[1]);
                     const float d0s = fmaf(qr[0], qr[0], fmaf(qr[1], qr[1], qr[2] * qr[2]));
-                    float b1 = d0s, b2 = 3e38f, bx = 0.f, by = 0.f, bz = 0.f, rho = 0.f;
-                    int bk = -1;
-                    auto coords = [&](int k, float* c) {
-#pragma unroll
-                        for (int a = 0; a < 3; ++a) {
-                            const int p = 4 + 3 * k + a;   // int16 slot (2 header dwords = 4 slots)
-                            c[a] = (float)((p & 1) ? ((int)w[p >> 1] >> 16) : (((int)(w[p >> 1] << 16)) >> 16));
+                    float b1 = d0s, b2 = 3e38f;
+                    int bk = -1;               // the winner's entry (-1: the node itself) ...
+                    uint32_t wa = 0u, wb = 0u; // ... and its two dwords (offset and index delta)
+                    uint32_t xb[10];           // entries kGraphLineA .. (nbx), read last
+                    // entry k's two dwords: 3 int16 offsets, then the int16 index delta
+                    auto dwords = [&](int k, uint32_t& a, uint32_t& b) {
+                        if (k < kGraphLineA) {
+                            a = w[2 + 2 * k];
+                            b = w[3 + 2 * k];
+                        } else {
+                            a = xb[2 * (k - kGraphLineA)];
+                            b = xb[2 * (k - kGraphLineA) + 1];
                         }
+                    };
+                    auto coords = [&](int k, float* c) {
+                        uint32_t a, b;
+                        dwords(k, a, b);
+                        c[0] = (float)(((int)(a << 16)) >> 16);
+                        c[1] = (float)((int)a >> 16);
+                        c[2] = (float)(((int)(b << 16)) >> 16);
                     };
                     // the winner so far and the runner-up (non-negative floats order like their bits: the
                     // runner-up is the median of {winner, runner-up, new}, one v_med3_u32, no NaN canonicalisation)
-                    auto upd = [&](float dd, float dx, float dy, float dz, int k) {
+                    auto upd = [&](float dd, int k) {
                         const unsigned ud = __float_as_uint(dd), u1 = __float_as_uint(b1);
                         const bool lt = ud < u1;
                         b2 = __uint_as_float(umed3(u1, __float_as_uint(b2), ud));
                         b1 = __uint_as_float(min(u1, ud));
                         if (lt) {
                             bk = k;
-                            bx = dx;
-                            by = dy;
-                            bz = dz;
+                            dwords(k, wa, wb);
                         }
                     };
                     // (an unused entry repeats a real one, k_graph_pack: no validity test here)
@@ -1661,11 +1677,7 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         const float dx = fmaf(-sc, c[0], qr[0]);
                         const float dy = fmaf(-sc, c[1], qr[1]);
                         const float dz = fmaf(-sc, c[2], qr[2]);
-                        upd(fmaf(dx, dx, fmaf(dy, dy, dz * dz)), dx, dy, dz, k);
-                        if (k == kRowSplit - 1) {   // |offset| of the first half's last entry (quantised)
-                            const float ox = sc * c[0], oy = sc * c[1], oz = sc * c[2];
-                            rho = __builtin_amdgcn_sqrtf(fmaf(ox, ox, fmaf(oy, oy, oz * oz)));
-                        }
+                        upd(fmaf(dx, dx, fmaf(dy, dy, dz * dz)), k);
                     };
                     // entries k and k + 1 on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: half the distance VALU)
                     auto entry2 = [&](int k) {
@@ -1677,30 +1689,63 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                         const f2v dy = __builtin_elementwise_fma(ms, f2v{ca[1], cb[1]}, f2v{qr[1], qr[1]});
                         const f2v dz = __builtin_elementwise_fma(ms, f2v{ca[2], cb[2]}, f2v{qr[2], qr[2]});
                         const f2v dd = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-                        upd(dd.x, dx.x, dy.x, dz.x, k);
-                        upd(dd.y, dx.y, dy.y, dz.y, k + 1);
+                        upd(dd.x, k);
+                        upd(dd.y, k + 1);
                     };
+                    auto entries = [&](int k0, int k1) {   // entries k0 .. k1 - 1
 #pragma unroll
-                    for (int k = 0; k + 1 < kRowSplit; k += 2) entry2(k);
-                    if (kRowSplit & 1) entry(kRowSplit - 1);
+                        for (int k = k0; k + 1 < k1; k += 2) entry2(k);
+                        if ((k1 - k0) & 1) entry(k1 - 1);
+                    };
+                    // |offset| of entry k (quantised): every later entry lies at >= it - s from the node
+                    auto reach = [&](int k) -> float {
+                        float c[3];
+                        coords(k, c);
+                        const float ox = sc * c[0], oy = sc * c[1], oz = sc * c[2];
+                        return __builtin_amdgcn_sqrtf(fmaf(ox, ox, fmaf(oy, oy, oz * oz)));
+                    };
+                    entries(0, kGraphHalf);
                     const float d0 = __builtin_amdgcn_sqrtf(d0s);
                     // distance error: qr's, an entry's quantisation (<= s/2 per axis), the arithmetic
                     const float e = eq + 0.87f * sc + kGraphErr * (d0 + r);
-                    // The row is sorted nearest-first (k_graph_pack): every entry of the second half lies at
-                    // >= rho - s from the node (quantisation), so at >= rho - s - d0 - e from p' and screens
-                    // >= lc.  It is read only by lanes where such an entry could still be the nearest or
-                    // within the tie band of it; elsewhere lc bounds the runner-up (sound for the gap).
-                    const float lc = rho - sc - d0 - 2.f * e;
-                    const bool need2 = lc <= __builtin_amdgcn_sqrtf(b1) + 2.f * e;
-                    if (wave_any(need2)) {
-                        if (need2) {
+                    // The row is sorted nearest-first (k_graph_pack): every entry after entry k lies at
+                    // >= reach(k) - s from the node (quantisation), so at >= reach(k) - s - d0 - e from p' and
+                    // screens >= lc.  The rest of the row is read only by lanes where such an entry could
+                    // still be the nearest or within the tie band of it; elsewhere lc bounds the runner-up
+                    // (sound for the gap).
+                    float lc = reach(kGraphHalf - 1) - sc - d0 - 2.f * e;
+                    bool need = lc <= __builtin_amdgcn_sqrtf(b1) + 2.f * e;
+                    if (wave_any(need)) {
+                        if (need) {
                             load_half(4);
+                            entries(kGraphHalf, kGraphLineA);
+                            lc = reach(kGraphLineA - 1) - sc - d0 - 2.f * e;
+                            need = lc <= __builtin_amdgcn_sqrtf(b1) + 2.f * e;
+                        }
+                        if (wave_any(need)) {
+                            if (need) {
+                                const uint4* rx = tg.nbx + (int64_t)node * 3;
 #pragma unroll
-                            for (int k = kRowSplit; k + 1 < kGraphK; k += 2) entry2(k);
-                            if ((kGraphK - kRowSplit) & 1) entry(kGraphK - 1);
+                                for (int c = 0; c < 2; ++c) {
+                                    const uint4 v = rx[c];
+                                    xb[4 * c] = v.x;
+                                    xb[4 * c + 1] = v.y;
+                                    xb[4 * c + 2] = v.z;
+                                    xb[4 * c + 3] = v.w;
+                                }
+                                const uint2 v2 = *reinterpret_cast<const uint2*>(rx + 2);
+                                xb[8] = v2.x;
+                                xb[9] = v2.y;
+                                entries(kGraphLineA, kGraphK);
+                            }
                         }
                     }
-                    if (!need2) b2 = fminf(b2, lc * lc);
+                    if (!need) b2 = fminf(b2, lc * lc);
+                    // the winner's sorted index without reading nbi, unless its delta did not fit 16 bits
+                    auto next_index = [&]() -> int {
+                        const int bd = (int)wb >> 16;
+                        return bd != kGraphFar ? node + bd : tg.nbi[(int64_t)node * kGraphK + bk];
+                    };
                     const float e1 = __builtin_amdgcn_sqrtf(b1), e2 = __builtin_amdgcn_sqrtf(b2);
                     if (e2 - e1 <= 2.f * e) {
                         // near tie: if the row covers it (same test as below), the nearest is one of the
@@ -1713,18 +1758,22 @@ __global__ void __launch_bounds__(64 * kCorrWaves) GICP_CORR_ATTR k_corr(CorrArg
                     } else if (d0 + e1 + 2.f * e < r) {           // proof (e1 = d0 at a local minimum)
                         gcert = true;
                         GICP_OUT(h > 0 ? 3 : bk < 0 ? 1 : 2);
-                        cj = bk < 0 ? node : tg.nbi[(int64_t)node * kGraphK + bk];
+                        cj = bk < 0 ? node : next_index();
                         ggap = fminf(e2, r - d0) - e1 - 2.f * e;
                         act = false;
                     } else if (bk < 0) {
                         act = false;                              // local minimum without proof
                         GICP_WHY(1);
                     } else {                                      // hop: p' relative to the nearer candidate
-                        qr[0] = bx;
-                        qr[1] = by;
-                        qr[2] = bz;
+                        // (the winner's offset again from its dwords: the same fused multiply-adds as its
+                        // distance above)
+                        const float c0 = (float)(((int)(wa << 16)) >> 16), c1 = (float)((int)wa >> 16);
+                        const float c2 = (float)(((int)(wb << 16)) >> 16);
+                        qr[0] = fmaf(-sc, c0, qr[0]);
+                        qr[1] = fmaf(-sc, c1, qr[1]);
+                        qr[2] = fmaf(-sc, c2, qr[2]);
                         eq = e;
-                        node = tg.nbi[(int64_t)node * kGraphK + bk];
+                        node = next_index();
                     }
                 }
             }
@@ -3039,7 +3088,7 @@ hipError_t launch_graph_pack(const GraphArgs& a, hipStream_t st) {
     clear_foreign_error();
     if (a.cl.n <= 0) return hipSuccess;
     const unsigned gp = (unsigned)((a.cl.n + 255) / 256);
-    hipLaunchKernelGGL(k_graph_pack, dim3(gp), dim3(256), 0, st, a.nb, a.nbh, a.cl.n, a.nbq, a.nbi);
+    hipLaunchKernelGGL(k_graph_pack, dim3(gp), dim3(256), 0, st, a.nb, a.nbh, a.cl.n, a.nbq, a.nbx, a.nbi);
     return hipGetLastError();
 }
 
