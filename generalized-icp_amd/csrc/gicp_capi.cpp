@@ -341,7 +341,7 @@ struct gicp_ctx {
     int moving_iters = 5;             // (GICP_MOVING_ITERS)
     int src_tile = kTile;             // source points per tile at most: 64, 32 or 16 (GICP_SRC_TILE)
     double kappa_frac = 0.002;        // certificate gap resolved by the walk, fraction of d_c (GICP_CERT_KAPPA)
-    int sparse_max = 2;               // CorrArgs::sparse_max (GICP_SPARSE_WALK; 0: sparse waves walk like the rest)
+    int sparse_max = 4;               // CorrArgs::sparse_max (GICP_SPARSE_WALK; 0: sparse waves walk like the rest)
     int sparse_amb = 2;               // CorrArgs::sparse_amb (GICP_SPARSE_AMB; 0: every fp64 re-resolution wave-wide)
     // cloud-build scratch (synchronous builds) and per-source-tile arrays, grow-only (a frame stream
     // allocates once)
